@@ -1,0 +1,133 @@
+/*
+ * uplink_ec.h — C ABI of the MI355X erasure-coding engine that replaces the
+ * Reed-Solomon stripe loop of storj/uplink's private/eestream (+ the piece
+ * fan-out of private/ecclient).  Plain pointers and sizes only; every compute
+ * entry point runs on the GPU (HIP, gfx950).  There is no CPU fallback: if no
+ * GPU is usable, ec_create returns EC_ERR_DEVICE.
+ *
+ * Reference interface each export replaces (storj/uplink @ /root/reference):
+ *
+ *   ec_create / ec_destroy   eestream.NewFEC + eestream.NewRSScheme
+ *                            private/eestream/fec.go:15-17, rs.go:17-19
+ *                            (called from encode.go:69-87)
+ *   ec_required/total/share_size/stripe_size
+ *                            ErasureScheme.RequiredCount/TotalCount/
+ *                            ErasureShareSize/StripeSize   rs.go:47-61
+ *   ec_encode_single         ErasureScheme.EncodeSingle    scheme.go:18, rs.go:21-23
+ *                            (caller segmentupload/encode.go:58, eestream/encode.go:187)
+ *   ec_encode                ErasureScheme.Encode          scheme.go:15, rs.go:25-30
+ *   ec_rebuild               ErasureScheme.Rebuild         scheme.go:26, rs.go:40-45
+ *                            (caller stripe.go:410-412)
+ *   ec_decode                ErasureScheme.Decode          scheme.go:22, rs.go:32-38
+ *                            (caller stripe.go:407-408; layout unsafe_rs.go:38-46)
+ *   ec_encode_segments       batch form of EncodeSingle over every (piece, stripe)
+ *                            of whole segments: segmentupload/encode.go:39-75 driven
+ *                            by single.go:228-238 (pieceReader.PieceReader)
+ *   ec_rebuild_segments      batch form of the per-stripe Rebuild loop of
+ *                            StripeReader.ReadStripes  stripe.go:382-428
+ *   ec_strerror/ec_format_error  error texts of infectious / eestream
+ *
+ * Error codes map to the errors eestream's callers test:
+ *   EC_ERR_NUM_NEGATIVE  "num must be non-negative"   (segmentupload/encode_test.go:53)
+ *   EC_ERR_NUM_RANGE     "num must be less than %d"   (segmentupload/encode_test.go:63)
+ *   EC_ERR_NOT_ENOUGH_SHARES  infectious.NotEnoughShares (stripe.go:446-449)
+ *   EC_ERR_TOO_MANY_ERRORS    infectious.TooManyErrors   (stripe.go:446-449)
+ *
+ * Threading: an ec_ctx is immutable after ec_create except for internal
+ * caches guarded by a mutex; every export is reentrant (uplink calls
+ * EncodeSingle from up to 300 goroutines, private/testuplink/uplink.go:83).
+ * No pointer passed in is retained after a call returns (cgo rules);
+ * the *_segments calls are asynchronous on `stream` and the caller keeps the
+ * device buffers alive until the stream is synchronised.
+ */
+#ifndef UPLINK_EC_H
+#define UPLINK_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EC_OK 0
+#define EC_ERR_PARAMS (-1)            /* "requires 1 <= k <= n <= 256" */
+#define EC_ERR_NUM_NEGATIVE (-2)      /* "num must be non-negative" */
+#define EC_ERR_NUM_RANGE (-3)         /* "num must be less than %d" (n) */
+#define EC_ERR_INPUT_LENGTH (-4)      /* "input length must be a multiple of %d" (k) */
+#define EC_ERR_OUTPUT_LENGTH (-5)     /* "output length must be %d" */
+#define EC_ERR_NOT_ENOUGH_SHARES (-6) /* infectious.NotEnoughShares */
+#define EC_ERR_TOO_MANY_ERRORS (-7)   /* infectious.TooManyErrors */
+#define EC_ERR_INVALID_SHARE (-8)     /* "invalid share id: %d" */
+#define EC_ERR_SINGULAR (-9)          /* decode matrix not invertible */
+#define EC_ERR_INVALID_ARG (-10)      /* null pointer / bad size / layout */
+#define EC_ERR_DEVICE (-11)           /* HIP runtime error or no GPU */
+#define EC_ERR_UNSUPPORTED (-12)      /* outside the engine's limits */
+#define EC_ERR_SHARE_SIZE (-13)       /* shares of different lengths */
+
+/* flags for ec_encode_segments */
+#define EC_FLAG_PARITY_ONLY 0x1 /* write only the n-k parity pieces */
+
+typedef struct ec_ctx ec_ctx;
+typedef void *ec_stream; /* hipStream_t; NULL = the default stream */
+
+int ec_create(int k, int n, int erasure_share_size, ec_ctx **out);
+void ec_destroy(ec_ctx *ctx);
+
+int ec_required(const ec_ctx *ctx);
+int ec_total(const ec_ctx *ctx);
+int ec_share_size(const ec_ctx *ctx);
+int ec_stripe_size(const ec_ctx *ctx);
+/* copies the n x k generator matrix (row-major) into out (n*k bytes) */
+int ec_generator(const ec_ctx *ctx, uint8_t *out);
+
+const char *ec_strerror(int code);
+/* message with the %d filled from ctx (n for NUM_RANGE, k for INPUT_LENGTH,
+ * `arg` for OUTPUT_LENGTH / INVALID_SHARE); returns the message length */
+int ec_format_error(const ec_ctx *ctx, int code, long long arg, char *buf, size_t len);
+
+/* ---- ErasureScheme surface: host buffers, synchronous, GPU-computed ---- */
+
+/* out (len(in)/k bytes) = erasure share `num` of the stripe `in` */
+int ec_encode_single(const ec_ctx *ctx, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len, int num);
+/* all n shares of `in`: share i written to out + i*(in_len/k) */
+int ec_encode(const ec_ctx *ctx, const uint8_t *in, size_t in_len, uint8_t *out);
+/* Rebuild: `nums` (nshares entries) is sorted in place together with
+ * `shares`, exactly as infectious sorts its []Share; the k data shares are
+ * written to out + i*share_len. */
+int ec_rebuild(const ec_ctx *ctx, int nshares, int *nums, const uint8_t **shares, size_t share_len, uint8_t *out);
+/* Decode: Correct (Berlekamp-Welch when nshares > k) + Rebuild; `shares`
+ * are corrected in place like infectious' share.Data.  out = k*share_len. */
+int ec_decode(const ec_ctx *ctx, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out);
+
+/* ---- batched, device-resident (HIP device pointers), async on stream ---- */
+
+/* segs: nseg padded segments, each nstripes*k*ess bytes, stripe-major
+ *       [stripe][k][ess] (the PadReader output of single.go:234-236).
+ * pieces: [nseg][n][nstripes*ess]  (or [nseg][n-k][...] with
+ *       EC_FLAG_PARITY_ONLY).  Piece i of a segment = the concatenation of
+ *       EncodeSingle(stripe, num=i) over its stripes. */
+int ec_encode_segments(const ec_ctx *ctx, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                       int flags, ec_stream stream);
+/* Rebuild whole segments from nshares >= k pieces (each nstripes*ess bytes,
+ * device pointers in `pieces`, piece numbers in `nums`, any order).  The
+ * share choice follows infectious Rebuild; out = nstripes*k*ess bytes,
+ * stripe-major.  nseg segments may be batched with strides (in bytes,
+ * 0 when nseg == 1). */
+int ec_rebuild_segments(const ec_ctx *ctx, int nshares, const int *nums, const uint8_t *const *pieces,
+                        size_t nstripes, uint8_t *out, ec_stream stream);
+int ec_rebuild_segments_batched(const ec_ctx *ctx, int nshares, const int *nums, const uint8_t *const *pieces,
+                                size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
+                                uint8_t *out, ec_stream stream);
+
+/* ---- device helpers ---- */
+int ec_device_count(void);
+int ec_set_device(int device);
+/* name of the kernel ec_encode_segments uses for this ctx ("special"/"generic"/"bytes") */
+const char *ec_encode_kernel_name(const ec_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UPLINK_EC_H */

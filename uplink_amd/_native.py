@@ -1,0 +1,88 @@
+"""ctypes binding of libuplink_ec.so (include/uplink_ec.h).
+
+The product path: every call below runs on the GPU.  If the shared library is
+missing or no GPU is usable the calls raise — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libuplink_ec.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "uplink_ec.h")
+
+EC_OK = 0
+EC_ERR_PARAMS = -1
+EC_ERR_NUM_NEGATIVE = -2
+EC_ERR_NUM_RANGE = -3
+EC_ERR_INPUT_LENGTH = -4
+EC_ERR_OUTPUT_LENGTH = -5
+EC_ERR_NOT_ENOUGH_SHARES = -6
+EC_ERR_TOO_MANY_ERRORS = -7
+EC_ERR_INVALID_SHARE = -8
+EC_ERR_SINGULAR = -9
+EC_ERR_INVALID_ARG = -10
+EC_ERR_DEVICE = -11
+EC_ERR_UNSUPPORTED = -12
+EC_ERR_SHARE_SIZE = -13
+
+EC_FLAG_PARITY_ONLY = 0x1
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must list every symbol include/uplink_ec.h declares
+SIGNATURES = {
+    "ec_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+    "ec_destroy": (None, [vp]),
+    "ec_required": (ctypes.c_int, [vp]),
+    "ec_total": (ctypes.c_int, [vp]),
+    "ec_share_size": (ctypes.c_int, [vp]),
+    "ec_stripe_size": (ctypes.c_int, [vp]),
+    "ec_generator": (ctypes.c_int, [vp, vp]),
+    "ec_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "ec_format_error": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_longlong, ctypes.c_char_p, ctypes.c_size_t]),
+    "ec_encode_single": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.c_int]),
+    "ec_encode": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
+    "ec_rebuild": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                  ctypes.c_size_t, vp]),
+    "ec_decode": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                 ctypes.c_size_t, vp]),
+    "ec_encode_segments": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, ctypes.c_int, vp]),
+    "ec_rebuild_segments": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                           ctypes.c_size_t, vp, vp]),
+    "ec_rebuild_segments_batched": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                   ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_size_t,
+                                                   ctypes.c_longlong, ctypes.c_longlong, vp, vp]),
+    "ec_device_count": (ctypes.c_int, []),
+    "ec_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "ec_encode_kernel_name": (ctypes.c_char_p, [vp]),
+}
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libuplink_ec.so; raises if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def strerror(code: int) -> str:
+    return load().ec_strerror(code).decode()

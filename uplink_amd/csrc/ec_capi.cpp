@@ -1,0 +1,639 @@
+// C ABI (include/uplink_ec.h) over the HIP stripe kernels.
+//
+// Host-side responsibilities only: argument validation with the reference's
+// error semantics, the choice of the k shares a Rebuild uses (infectious'
+// sort + front/back rule), the k x k inversion of
+// the decode matrix (once per share set, cached), and staging of
+// host buffers for the per-stripe ErasureScheme calls.  Every byte of share
+// data is produced by a GPU kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <list>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/uplink_ec.h"
+#include "gf256.hpp"
+#include "rs_correct.hpp"
+#include "rs_kernels.hpp"
+
+using namespace uplink_ec;
+
+namespace {
+
+struct DecodePlan {
+    std::vector<int> ids;      // chosen share numbers, position i = infectious row i
+    std::vector<int> missing;  // positions i (== data number) rebuilt
+    uint8_t *d_coef = nullptr; // [c][r] = Dinv[missing[r]][c], ld = coef_ld
+    int coef_ld = 0;
+    ~DecodePlan() {
+        // hipFree synchronises with outstanding device work before releasing
+        if (d_coef) (void)hipFree(d_coef);
+    }
+};
+using PlanPtr = std::shared_ptr<DecodePlan>;
+
+struct Workspace {
+    uint8_t *d_buf = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+};
+
+}  // namespace
+
+struct ec_ctx {
+    int k = 0, n = 0, ess = 0, device = 0;
+    std::vector<uint8_t> G;        // n x k
+    uint8_t *d_coef_all = nullptr; // [j][i] = G[i][j], ld = ld_all
+    int ld_all = 0;
+    std::mutex mu;
+    std::list<PlanPtr> plans;      // MRU first
+    std::vector<Workspace *> free_ws;
+    std::vector<std::unique_ptr<Workspace>> all_ws;
+};
+
+namespace {
+
+constexpr size_t kMaxPlans = 64;
+
+int round16(int x) { return (x + 15) & ~15; }
+
+int hip_fail(hipError_t e) {
+    if (e == hipSuccess) return EC_OK;
+    fprintf(stderr, "uplink_ec: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
+    return EC_ERR_DEVICE;
+}
+
+#define HIP_TRY(x)                                   \
+    do {                                             \
+        hipError_t e_ = (x);                         \
+        if (e_ != hipSuccess) return hip_fail(e_);   \
+    } while (0)
+
+Workspace *acquire_ws(ec_ctx *c, size_t need) {
+    Workspace *w = nullptr;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (!c->free_ws.empty()) {
+            w = c->free_ws.back();
+            c->free_ws.pop_back();
+        } else {
+            c->all_ws.emplace_back(new Workspace());
+            w = c->all_ws.back().get();
+        }
+    }
+    if (!w->stream && hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) w->stream = nullptr;
+    if (w->cap < need) {
+        if (w->d_buf) (void)hipFree(w->d_buf);
+        w->d_buf = nullptr;
+        w->cap = 0;
+        size_t cap = std::max(need, (size_t)1 << 20);
+        if (hipMalloc(&w->d_buf, cap) == hipSuccess) w->cap = cap;
+    }
+    return w;
+}
+
+void release_ws(ec_ctx *c, Workspace *w) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->free_ws.push_back(w);
+}
+
+void fill_geometry(RsArgs &a, int ess, int64_t nstripes, int64_t nseg) {
+    a.ess = ess;
+    a.cps = ess / 16;
+    a.nstripes = nstripes;
+    a.chunks_per_seg = nstripes * (ess / 16);
+    a.tiles_per_seg = (a.chunks_per_seg + 127) / 128;
+    a.total_tiles = a.tiles_per_seg * nseg;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// Launch a matrix product described by `a` (rows a.nout, possibly > kMaxOps:
+// split into several launches; copies happen in the first one only).
+int run_matmul(RsArgs a, int64_t nseg, bool bitsliced, hipStream_t s) {
+    const int total_rows = a.nout;
+    int64_t out_off_all[256];
+    for (int r = 0; r < total_rows; r++) out_off_all[r] = a.out_off[r];
+    const uint8_t *coef0 = a.coef;
+    int done = 0;
+    bool first = true;
+    do {
+        const int rows = std::min(kMaxOps, total_rows - done);
+        a.nout = rows;
+        for (int r = 0; r < rows; r++) a.out_off[r] = out_off_all[done + r];
+        a.coef = coef0 + done;
+        if (!first)
+            for (int j = 0; j < a.nin; j++) a.copy_off[j] = -1;
+        if (bitsliced) {
+            HIP_TRY(launch_matmul_generic(a, 0, s));
+        } else {
+            const int64_t keep = a.total_tiles;
+            a.total_tiles = nseg;  // byte kernel: total_tiles carries the segment count
+            HIP_TRY(launch_matmul_bytes(a, s));
+            a.total_tiles = keep;
+        }
+        done += rows;
+        first = false;
+    } while (done < total_rows);
+    return EC_OK;
+}
+
+// infectious Rebuild share choice: sort by number, then for i in 0..k-1 take
+// the front share if its number == i else take from the back.
+int choose_shares(const ec_ctx *c, int nshares, const int *nums, std::vector<int> &order_out,
+                  std::vector<int> &ids_out) {
+    if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+    std::vector<int> order(nshares);
+    for (int i = 0; i < nshares; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return nums[a] < nums[b]; });
+    int b = 0, e = nshares - 1;
+    order_out.clear();
+    ids_out.clear();
+    for (int i = 0; i < c->k; i++) {
+        int pick;
+        if (nums[order[b]] == i) pick = order[b++];
+        else pick = order[e--];
+        if (nums[pick] >= c->n || nums[pick] < 0) return EC_ERR_INVALID_SHARE;
+        order_out.push_back(pick);
+        ids_out.push_back(nums[pick]);
+    }
+    return EC_OK;
+}
+
+// Decode plan for the chosen ids (cached per share set).
+int get_plan(ec_ctx *c, const std::vector<int> &ids, PlanPtr *out) {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        for (auto it = c->plans.begin(); it != c->plans.end(); ++it) {
+            if ((*it)->ids == ids) {
+                c->plans.splice(c->plans.begin(), c->plans, it);
+                *out = c->plans.front();
+                return EC_OK;
+            }
+        }
+    }
+    const int k = c->k;
+    std::vector<uint8_t> m((size_t)k * k, 0);
+    for (int i = 0; i < k; i++) {
+        if (ids[i] < k) m[(size_t)i * k + i] = 1;
+        else memcpy(&m[(size_t)i * k], &c->G[(size_t)ids[i] * k], k);
+    }
+    if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
+    PlanPtr p = std::make_shared<DecodePlan>();
+    p->ids = ids;
+    for (int i = 0; i < k; i++)
+        if (ids[i] >= k) p->missing.push_back(i);
+    const int R = (int)p->missing.size();
+    p->coef_ld = round16(std::max(R, 1));
+    std::vector<uint8_t> coef((size_t)k * p->coef_ld, 0);
+    for (int r = 0; r < R; r++)
+        for (int col = 0; col < k; col++) coef[(size_t)col * p->coef_ld + r] = m[(size_t)p->missing[r] * k + col];
+    HIP_TRY(hipMalloc(&p->d_coef, coef.size()));
+    HIP_TRY(hipMemcpy(p->d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice));
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->plans.push_front(p);
+        while (c->plans.size() > kMaxPlans) c->plans.pop_back();
+    }
+    *out = p;
+    return EC_OK;
+}
+
+// Core rebuild: device pointers of the nshares pieces, nstripes stripes of
+// share size `ess`, out stripe-major; batched over nseg with strides.
+int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int ess, int64_t nstripes,
+                   int64_t nseg, int64_t piece_seg_stride, int64_t out_seg_stride, uint8_t *out, hipStream_t s) {
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    PlanPtr plan;
+    rc = get_plan(c, ids, &plan);
+    if (rc) return rc;
+    const int k = c->k;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    RsArgs a{};
+    const uint8_t *base = pieces[order[0]];
+    for (int i = 0; i < k; i++) base = std::min(base, pieces[order[i]]);
+    a.in_base = base;
+    a.out_base = out;
+    a.coef = plan->d_coef;
+    a.coef_ld = plan->coef_ld;
+    a.in_stripe_stride = ess;
+    a.out_stripe_stride = (int64_t)k * ess;
+    a.in_seg_stride = piece_seg_stride;
+    a.out_seg_stride = out_seg_stride;
+    a.nin = k;
+    a.nout = (int)plan->missing.size();
+    bool bits = (ess % 16) == 0 && aligned16(out);
+    for (int i = 0; i < k; i++) {
+        const uint8_t *p = pieces[order[i]];
+        a.in_off[i] = p - base;
+        a.copy_off[i] = ids[i] < k ? (int64_t)ids[i] * ess : -1;
+        bits = bits && aligned16(p);
+    }
+    for (int r = 0; r < a.nout; r++) a.out_off[r] = (int64_t)plan->missing[r] * ess;
+    fill_geometry(a, ess, nstripes, nseg);
+    if (!bits) a.cps = 1;
+    return run_matmul(a, nseg, bits, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ec_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ec_set_device(int device) { return hip_fail(hipSetDevice(device)); }
+
+int ec_create(int k, int n, int ess, ec_ctx **out) {
+    if (!out) return EC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (k <= 0 || n <= 0 || k > 256 || n > 256 || k > n) return EC_ERR_PARAMS;
+    if (ess <= 0) return EC_ERR_INVALID_ARG;
+    if (ec_device_count() <= 0) {
+        fprintf(stderr, "uplink_ec: no HIP device available\n");
+        return EC_ERR_DEVICE;
+    }
+    std::unique_ptr<ec_ctx> c(new ec_ctx());
+    c->k = k;
+    c->n = n;
+    c->ess = ess;
+    HIP_TRY(hipGetDevice(&c->device));
+    c->G.resize((size_t)n * k);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < k; j++) c->G[(size_t)i * k + j] = gen_entry(k, i, j);
+    c->ld_all = round16(n);
+    std::vector<uint8_t> coef((size_t)k * c->ld_all, 0);
+    for (int j = 0; j < k; j++)
+        for (int i = 0; i < n; i++) coef[(size_t)j * c->ld_all + i] = c->G[(size_t)i * k + j];
+    HIP_TRY(hipMalloc(&c->d_coef_all, coef.size()));
+    HIP_TRY(hipMemcpy(c->d_coef_all, coef.data(), coef.size(), hipMemcpyHostToDevice));
+    *out = c.release();
+    return EC_OK;
+}
+
+void ec_destroy(ec_ctx *c) {
+    if (!c) return;
+    c->plans.clear();
+    for (auto &w : c->all_ws) {
+        if (w->stream) (void)hipStreamSynchronize(w->stream), (void)hipStreamDestroy(w->stream);
+        if (w->d_buf) (void)hipFree(w->d_buf);
+    }
+    if (c->d_coef_all) (void)hipFree(c->d_coef_all);
+    delete c;
+}
+
+int ec_required(const ec_ctx *c) { return c ? c->k : EC_ERR_INVALID_ARG; }
+int ec_total(const ec_ctx *c) { return c ? c->n : EC_ERR_INVALID_ARG; }
+int ec_share_size(const ec_ctx *c) { return c ? c->ess : EC_ERR_INVALID_ARG; }
+int ec_stripe_size(const ec_ctx *c) { return c ? c->ess * c->k : EC_ERR_INVALID_ARG; }
+
+int ec_generator(const ec_ctx *c, uint8_t *out) {
+    if (!c || !out) return EC_ERR_INVALID_ARG;
+    memcpy(out, c->G.data(), c->G.size());
+    return EC_OK;
+}
+
+const char *ec_strerror(int code) {
+    switch (code) {
+        case EC_OK: return "ok";
+        case EC_ERR_PARAMS: return "requires 1 <= k <= n <= 256";
+        case EC_ERR_NUM_NEGATIVE: return "num must be non-negative";
+        case EC_ERR_NUM_RANGE: return "num must be less than %d";
+        case EC_ERR_INPUT_LENGTH: return "input length must be a multiple of %d";
+        case EC_ERR_OUTPUT_LENGTH: return "output length must be %d";
+        case EC_ERR_NOT_ENOUGH_SHARES: return "not enough shares";
+        case EC_ERR_TOO_MANY_ERRORS: return "too many errors to reconstruct";
+        case EC_ERR_INVALID_SHARE: return "invalid share id: %d";
+        case EC_ERR_SINGULAR: return "matrix is singular";
+        case EC_ERR_INVALID_ARG: return "invalid argument";
+        case EC_ERR_DEVICE: return "HIP device error";
+        case EC_ERR_UNSUPPORTED: return "unsupported parameters";
+        case EC_ERR_SHARE_SIZE: return "shares must all have the same length";
+        default: return "unknown error";
+    }
+}
+
+int ec_format_error(const ec_ctx *c, int code, long long arg, char *buf, size_t len) {
+    const char *fmt = ec_strerror(code);
+    long long v = arg;
+    if (code == EC_ERR_NUM_RANGE && c) v = c->n;
+    if (code == EC_ERR_INPUT_LENGTH && c) v = c->k;
+    int r = snprintf(buf, len, fmt, v);
+    return r;
+}
+
+const char *ec_encode_kernel_name(const ec_ctx *c) {
+    if (!c) return "";
+    if (c->ess % 16) return "bytes";
+    return have_special_encoder(c->k, c->n) ? "special" : "generic";
+}
+
+int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                       int flags, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    const int k = c->k, n = c->n, ess = c->ess;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
+    const int64_t piece_len = (int64_t)nstripes * ess;
+    RsArgs a{};
+    a.in_base = segs;
+    a.out_base = pieces;
+    a.coef = c->d_coef_all + k;  // parity rows k..n-1
+    a.coef_ld = c->ld_all;
+    a.in_stripe_stride = (int64_t)k * ess;
+    a.out_stripe_stride = ess;
+    a.in_seg_stride = (int64_t)nstripes * k * ess;
+    a.out_seg_stride = (int64_t)(parity_only ? n - k : n) * piece_len;
+    a.nin = k;
+    a.nout = n - k;
+    for (int j = 0; j < k; j++) {
+        a.in_off[j] = (int64_t)j * ess;
+        a.copy_off[j] = parity_only ? -1 : (int64_t)j * piece_len;
+    }
+    int64_t out_off[256];
+    for (int r = 0; r < n - k; r++) out_off[r] = (int64_t)(parity_only ? r : k + r) * piece_len;
+    for (int r = 0; r < std::min(n - k, kMaxOps); r++) a.out_off[r] = out_off[r];
+    fill_geometry(a, ess, (int64_t)nstripes, (int64_t)nseg);
+    const bool bits = (ess % 16) == 0 && aligned16(segs) && aligned16(pieces);
+    if (bits && have_special_encoder(k, n)) {
+        HIP_TRY(launch_encode_special(k, n, a, 0, s));
+        return EC_OK;
+    }
+    if (!bits) a.cps = 1;
+    // rows beyond kMaxOps are handled by run_matmul's split
+    if (n - k > kMaxOps) {
+        // run_matmul reads a.out_off for all rows: pass through a widened copy
+        RsArgs b = a;
+        int done = 0;
+        bool first = true;
+        while (done < n - k) {
+            const int rows = std::min(kMaxOps, n - k - done);
+            b.nout = rows;
+            b.coef = c->d_coef_all + k + done;
+            for (int r = 0; r < rows; r++) b.out_off[r] = out_off[done + r];
+            if (!first)
+                for (int j = 0; j < k; j++) b.copy_off[j] = -1;
+            int rc = run_matmul(b, (int64_t)nseg, bits, s);
+            if (rc) return rc;
+            done += rows;
+            first = false;
+        }
+        return EC_OK;
+    }
+    return run_matmul(a, (int64_t)nseg, bits, s);
+}
+
+int ec_rebuild_segments_batched(const ec_ctx *cc, int nshares, const int *nums, const uint8_t *const *pieces,
+                                size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
+                                uint8_t *out, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !nums || !pieces || !out) return EC_ERR_INVALID_ARG;
+    if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+    if (nstripes == 0 || nseg == 0) return EC_OK;
+    return rebuild_device(c, nshares, nums, pieces, c->ess, (int64_t)nstripes, (int64_t)nseg, piece_seg_stride,
+                          out_seg_stride, out, (hipStream_t)stream);
+}
+
+int ec_rebuild_segments(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces,
+                        size_t nstripes, uint8_t *out, ec_stream stream) {
+    return ec_rebuild_segments_batched(c, nshares, nums, pieces, nstripes, 1, 0, 0, out, stream);
+}
+
+// ---------------------------------------------------------------- per-stripe
+int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len, int num) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c) return EC_ERR_INVALID_ARG;
+    if (num < 0) return EC_ERR_NUM_NEGATIVE;
+    if (num >= c->n) return EC_ERR_NUM_RANGE;
+    if (in_len % (size_t)c->k) return EC_ERR_INPUT_LENGTH;
+    const size_t bs = in_len / c->k;
+    if (out_len != bs) return EC_ERR_OUTPUT_LENGTH;
+    if (bs == 0) return EC_OK;
+    if (!in || !out) return EC_ERR_INVALID_ARG;
+    if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    Workspace *w = acquire_ws(c, in_len + bs + 64);
+    if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
+    const size_t out_at = (in_len + 15) & ~(size_t)15;
+    int rc = EC_OK;
+    do {
+        if (hipMemcpyAsync(w->d_buf, in, in_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        RsArgs a{};
+        a.in_base = w->d_buf;
+        a.out_base = w->d_buf + out_at;
+        a.coef = c->d_coef_all + num;
+        a.coef_ld = c->ld_all;
+        a.in_stripe_stride = (int64_t)in_len;
+        a.out_stripe_stride = (int64_t)bs;
+        a.nin = c->k;
+        a.nout = 1;
+        for (int j = 0; j < c->k; j++) { a.in_off[j] = (int64_t)j * bs; a.copy_off[j] = -1; }
+        a.out_off[0] = 0;
+        fill_geometry(a, (int)bs, 1, 1);
+        const bool bits = (bs % 16) == 0;
+        if (!bits) a.cps = 1;
+        rc = run_matmul(a, 1, bits, w->stream);
+        if (rc) break;
+        if (hipMemcpyAsync(out, w->d_buf + out_at, bs, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
+    } while (0);
+    release_ws(c, w);
+    return rc;
+}
+
+int ec_encode(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c) return EC_ERR_INVALID_ARG;
+    if (in_len % (size_t)c->k) return EC_ERR_INPUT_LENGTH;
+    const size_t bs = in_len / c->k;
+    if (bs == 0) return EC_OK;
+    if (!in || !out) return EC_ERR_INVALID_ARG;
+    const size_t out_at = (in_len + 15) & ~(size_t)15;
+    Workspace *w = acquire_ws(c, out_at + bs * c->n + 64);
+    if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
+    int rc = EC_OK;
+    do {
+        if (hipMemcpyAsync(w->d_buf, in, in_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        RsArgs a{};
+        a.in_base = w->d_buf;
+        a.out_base = w->d_buf + out_at;
+        a.coef = c->d_coef_all + c->k;
+        a.coef_ld = c->ld_all;
+        a.in_stripe_stride = (int64_t)in_len;
+        a.out_stripe_stride = (int64_t)bs;
+        a.nin = c->k;
+        a.nout = c->n - c->k;
+        for (int j = 0; j < c->k; j++) { a.in_off[j] = (int64_t)j * bs; a.copy_off[j] = (int64_t)j * bs; }
+        for (int r = 0; r < std::min(a.nout, kMaxOps); r++) a.out_off[r] = (int64_t)(c->k + r) * bs;
+        fill_geometry(a, (int)bs, 1, 1);
+        const bool bits = (bs % 16) == 0;
+        if (!bits) a.cps = 1;
+        if (a.nout > kMaxOps || c->k > kMaxOps) { rc = EC_ERR_UNSUPPORTED; break; }
+        rc = run_matmul(a, 1, bits, w->stream);
+        if (rc) break;
+        if (hipMemcpyAsync(out, w->d_buf + out_at, bs * c->n, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
+    } while (0);
+    release_ws(c, w);
+    return rc;
+}
+
+static void sort_shares_inplace(int ns, int *nums, const uint8_t **shares) {
+    // stable insertion sort, like sort.Sort on a small []Share
+    for (int a = 1; a < ns; a++) {
+        int kn = nums[a];
+        const uint8_t *kd = shares[a];
+        int b = a - 1;
+        while (b >= 0 && nums[b] > kn) {
+            nums[b + 1] = nums[b];
+            shares[b + 1] = shares[b];
+            b--;
+        }
+        nums[b + 1] = kn;
+        shares[b + 1] = kd;
+    }
+}
+
+int ec_rebuild(const ec_ctx *cc, int nshares, int *nums, const uint8_t **shares, size_t share_len, uint8_t *out) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
+    if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+    sort_shares_inplace(nshares, nums, shares);
+    if (share_len == 0) return EC_OK;
+    if (!out) return EC_ERR_INVALID_ARG;
+    const size_t slot = (share_len + 15) & ~(size_t)15;
+    const size_t out_at = slot * nshares;
+    Workspace *w = acquire_ws(c, out_at + share_len * c->k + 64);
+    if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
+    int rc = EC_OK;
+    do {
+        std::vector<const uint8_t *> dptr(nshares);
+        for (int i = 0; i < nshares; i++) {
+            if (hipMemcpyAsync(w->d_buf + slot * i, shares[i], share_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            dptr[i] = w->d_buf + slot * i;
+        }
+        if (rc) break;
+        rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, w->d_buf + out_at, w->stream);
+        if (rc) break;
+        if (hipMemcpyAsync(out, w->d_buf + out_at, share_len * c->k, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
+    } while (0);
+    release_ws(c, w);
+    return rc;
+}
+
+// Decode = Correct + Rebuild (rsScheme.Decode, rs.go:32-38).  Correct: the
+// shares beyond the first k (sorted) are re-encoded from the first k on the
+// GPU, mismatching byte columns are flagged, and each flagged column is
+// corrected by Berlekamp-Welch on the GPU; shares are corrected in place.
+int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
+    const int k = c->k;
+    if (nshares < k) return EC_ERR_NOT_ENOUGH_SHARES;
+    sort_shares_inplace(nshares, nums, (const uint8_t **)shares);
+    if (share_len == 0) return EC_OK;
+    if (!out) return EC_ERR_INVALID_ARG;
+    for (int i = 0; i < nshares; i++)
+        if (nums[i] < 0 || nums[i] >= c->n) return EC_ERR_INVALID_SHARE;
+    if (k > kMaxOps || nshares - k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    const size_t slot = (share_len + 15) & ~(size_t)15;
+    const int extra = nshares - k;
+    const size_t exp_at = slot * nshares;
+    const size_t flags_at = exp_at + slot * (size_t)extra;
+    const size_t cols_at = (flags_at + slot + 15) & ~(size_t)15;
+    const size_t nums_at = cols_at + share_len * 8;
+    const size_t stat_at = nums_at + 4 * 256;
+    const size_t out_at = (stat_at + share_len * 4 + 15) & ~(size_t)15;
+    Workspace *w = acquire_ws(c, out_at + share_len * k + 64);
+    if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
+    int rc = EC_OK;
+    uint8_t *d = w->d_buf;
+    do {
+        for (int i = 0; i < nshares; i++)
+            if (hipMemcpyAsync(d + slot * i, shares[i], share_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (rc) break;
+        if (extra > 0) {
+            // T = G[others] * inverse(G[first k])
+            std::vector<uint8_t> m((size_t)k * k);
+            for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[i] * k], k);
+            if (!gf_invert(m.data(), k)) { rc = EC_ERR_SINGULAR; break; }
+            const int ld = round16(extra);
+            std::vector<uint8_t> coef((size_t)k * ld, 0);
+            for (int r = 0; r < extra; r++)
+                for (int col = 0; col < k; col++) {
+                    uint8_t acc = 0;
+                    for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[k + r] * k + t], m[(size_t)t * k + col]);
+                    coef[(size_t)col * ld + r] = acc;
+                }
+            uint8_t *d_coef = nullptr;
+            if (hipMalloc(&d_coef, coef.size()) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            std::unique_ptr<uint8_t, void (*)(uint8_t *)> coef_guard(d_coef, [](uint8_t *p) { (void)hipFree(p); });
+            if (hipMemcpyAsync(d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            RsArgs a{};
+            a.in_base = d;
+            a.out_base = d + exp_at;
+            a.coef = d_coef;
+            a.coef_ld = ld;
+            a.in_stripe_stride = (int64_t)share_len;
+            a.out_stripe_stride = (int64_t)share_len;
+            a.nin = k;
+            a.nout = extra;
+            for (int j = 0; j < k; j++) { a.in_off[j] = (int64_t)slot * j; a.copy_off[j] = -1; }
+            for (int r = 0; r < extra; r++) a.out_off[r] = (int64_t)slot * r;
+            fill_geometry(a, (int)share_len, 1, 1);
+            const bool bits = (share_len % 16) == 0;
+            if (!bits) a.cps = 1;
+            rc = run_matmul(a, 1, bits, w->stream);
+            if (rc) break;
+            if (launch_flag_columns(d, slot, d + exp_at, slot, k, nshares, share_len, d + flags_at, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            std::vector<uint8_t> flags(share_len);
+            if (hipMemcpyAsync(flags.data(), d + flags_at, share_len, hipMemcpyDeviceToHost, w->stream) != hipSuccess ||
+                hipStreamSynchronize(w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            std::vector<int64_t> cols;
+            for (size_t col = 0; col < share_len; col++)
+                if (flags[col]) cols.push_back((int64_t)col);
+            if (!cols.empty()) {
+                if (hipMemcpyAsync(d + cols_at, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, w->stream) != hipSuccess ||
+                    hipMemcpyAsync(d + nums_at, nums, 4 * (size_t)nshares, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                if (launch_berlekamp_welch(d, slot, (const int *)(d + nums_at), k, c->n, nshares, (const int64_t *)(d + cols_at),
+                                           (int)cols.size(), (int *)(d + stat_at), w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                std::vector<int> status(cols.size());
+                if (hipMemcpyAsync(status.data(), d + stat_at, 4 * cols.size(), hipMemcpyDeviceToHost, w->stream) != hipSuccess ||
+                    hipStreamSynchronize(w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                for (int st : status) {
+                    if (st == -6) { rc = EC_ERR_NOT_ENOUGH_SHARES; break; }
+                    if (st == -7) { rc = EC_ERR_TOO_MANY_ERRORS; break; }
+                    if (st != 0) { rc = EC_ERR_UNSUPPORTED; break; }
+                }
+                if (rc) break;
+                for (int i = 0; i < nshares; i++)
+                    if (hipMemcpyAsync(shares[i], d + slot * i, share_len, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                if (rc) break;
+            }
+        }
+        std::vector<const uint8_t *> dptr(nshares);
+        for (int i = 0; i < nshares; i++) dptr[i] = d + slot * i;
+        rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, d + out_at, w->stream);
+        if (rc) break;
+        if (hipMemcpyAsync(out, d + out_at, share_len * k, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
+    } while (0);
+    if (rc) (void)hipStreamSynchronize(w->stream);
+    release_ws(c, w);
+    return rc;
+}
+
+}  // extern "C"
