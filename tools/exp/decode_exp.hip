@@ -1,0 +1,297 @@
+// Developer experiment (not product): runtime-matrix bodies for the rebuild
+// kernel, RS(29,80), 8 segments, worst-case share set {51..79} (m = 29) and a
+// random 29-subset.  Build: make -C tools/exp bin/decode_exp
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../../uplink_amd/csrc/rs_device.hpp"
+
+using namespace uplink_ec;
+using namespace uplink_ec::dev;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+// MODE 0: branchy bit pairs (product); 1: dense SGPR masks over the y chain;
+// 2: one branch per coefficient bit
+template <int OPW, int MODE>
+__device__ __forceinline__ void body(const RsArgs &a, const uint32_t *lds, int lane, int jbase, int jn, int rbase,
+                                     int cnt, uint32_t (&acc)[OPW][8]) {
+    if constexpr (MODE == 0) {
+        compute_generic<OPW>(a, lds, lane, jbase, jn, rbase, cnt, acc);
+        return;
+    }
+    for (int jj = 0; jj < jn; jj++) {
+        uint32_t y[8][8];
+#pragma unroll
+        for (int p = 0; p < 8; p++) y[0][p] = lds[(jj * 8 + p) * 64 + lane];
+#pragma unroll
+        for (int b = 1; b < 8; b++) mul2_planes(y[b - 1], y[b]);
+        const uint8_t *cp = a.coef + (int64_t)(jbase + jj) * a.coef_ld + rbase;
+        static_for<OPW / 4>([&]<int Q>() {
+            const uint32_t cw = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * Q));
+            static_for<4>([&]<int B>() {
+                constexpr int O = 4 * Q + B;
+                if (O < cnt) {
+                    const uint32_t cv = (cw >> (8 * B)) & 0xffu;
+                    if constexpr (MODE == 1) {
+#pragma unroll
+                        for (int b = 0; b < 8; b++) {
+                            const uint32_t m = __builtin_amdgcn_readfirstlane(0u - ((cv >> b) & 1u));
+#pragma unroll
+                            for (int p = 0; p < 8; p++)
+                                acc[O][p] = __builtin_amdgcn_bitop3_b32(acc[O][p], y[b][p], m, 0x6a);  // a ^ (b & c)
+                        }
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 8; b++) {
+                            if ((cv >> b) & 1u) {
+#pragma unroll
+                                for (int p = 0; p < 8; p++) acc[O][p] ^= y[b][p];
+                            }
+                        }
+                    }
+                }
+            });
+        });
+    }
+}
+
+template <int OPW, int MODE, int JC>
+__global__ __launch_bounds__(256, 2) void dec_plain(const RsArgs a) {
+    constexpr int NW = 4;
+    constexpr int PER = JC / NW;
+    __shared__ uint32_t lds[JC * 8 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int per_wave = (a.nout + NW - 1) / NW;
+    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const int64_t seg = tile / a.tiles_per_seg;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        const int rbase = wave * per_wave;
+        int cnt = a.nout - rbase;
+        cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
+        uint32_t acc[OPW][8];
+#pragma unroll
+        for (int o = 0; o < OPW; o++)
+#pragma unroll
+            for (int p = 0; p < 8; p++) acc[o][p] = 0;
+        for (int j0 = 0; j0 < a.nin; j0 += JC) {
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, true);
+            __syncthreads();
+            if (cnt > 0) body<OPW, MODE>(a, lds, lane, j0, jn, rbase, cnt, acc);
+            __syncthreads();
+        }
+        store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+    }
+}
+
+
+// two tiles (2 x 2048 columns) per WG item: each branch on a coefficient bit
+// guards 16 XORs instead of 8; multiples x*2^b formed on the fly.
+template <int OPW, int JC, int PAIRS>
+__global__ __launch_bounds__(256, 2) void dec_two(const RsArgs a) {
+    constexpr int NW = 4;
+    constexpr int PER = JC / NW;
+    __shared__ uint32_t lds[2][JC * 8 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int per_wave = (a.nout + NW - 1) / NW;
+    const int64_t npairs = (a.total_tiles + 1) / 2;
+    for (int64_t tp = blockIdx.x; tp < npairs; tp += gridDim.x) {
+        int64_t tiles[2] = {2 * tp, 2 * tp + 1};
+        TileCols c[2];
+        int64_t segs[2];
+        bool tv[2];
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            tv[w] = tiles[w] < a.total_tiles;
+            const int64_t t = tv[w] ? tiles[w] : tiles[0];
+            segs[w] = t / a.tiles_per_seg;
+            c[w] = tile_cols(a, t - segs[w] * a.tiles_per_seg, lane);
+            if (!tv[w]) { c[w].vA = false; c[w].vB = false; }
+        }
+        const int rbase = wave * per_wave;
+        int cnt = a.nout - rbase;
+        cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
+        uint32_t acc[2][OPW][8];
+#pragma unroll
+        for (int w = 0; w < 2; w++)
+#pragma unroll
+            for (int o = 0; o < OPW; o++)
+#pragma unroll
+                for (int p = 0; p < 8; p++) acc[w][o][p] = 0;
+        for (int j0 = 0; j0 < a.nin; j0 += JC) {
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            stage_inputs<NW, PER, true>(a, segs[0], c[0], lds[0], lane, wave, j0, jn, true);
+            stage_inputs<NW, PER, true>(a, segs[1], c[1], lds[1], lane, wave, j0, jn, true);
+            __syncthreads();
+            if (cnt > 0) {
+                for (int jj = 0; jj < jn; jj++) {
+                    uint32_t y[2][8];
+#pragma unroll
+                    for (int w = 0; w < 2; w++)
+#pragma unroll
+                        for (int p = 0; p < 8; p++) y[w][p] = lds[w][(jj * 8 + p) * 64 + lane];
+                    const uint8_t *cp = a.coef + (int64_t)(j0 + jj) * a.coef_ld + rbase;
+                    uint32_t cw[OPW / 4];
+#pragma unroll
+                    for (int q = 0; q < OPW / 4; q++) cw[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * q));
+                    if constexpr (PAIRS == 0) {
+#pragma unroll
+                        for (int b = 0; b < 8; b++) {
+                            static_for<OPW>([&]<int O>() {
+                                if (O < cnt) {
+                                    const uint32_t bitset = __builtin_amdgcn_readfirstlane((cw[O / 4] >> (8 * (O % 4) + b)) & 1u);
+                                    if (bitset) {
+#pragma unroll
+                                        for (int w = 0; w < 2; w++)
+#pragma unroll
+                                            for (int p = 0; p < 8; p++) acc[w][O][p] ^= y[w][p];
+                                    }
+                                }
+                            });
+                            if (b < 7) {
+#pragma unroll
+                                for (int w = 0; w < 2; w++) {
+                                    uint32_t n[8];
+                                    mul2_planes(y[w], n);
+#pragma unroll
+                                    for (int p = 0; p < 8; p++) y[w][p] = n[p];
+                                }
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < 4; g++) {
+                            uint32_t y2[2][8];
+#pragma unroll
+                            for (int w = 0; w < 2; w++) {
+                                mul2_planes(y[w], y2[w]);
+                            }
+                            static_for<OPW>([&]<int O>() {
+                                if (O < cnt) {
+                                    const uint32_t two = __builtin_amdgcn_readfirstlane((cw[O / 4] >> (8 * (O % 4) + 2 * g)) & 3u);
+                                    if (two == 3u) {
+#pragma unroll
+                                        for (int w = 0; w < 2; w++)
+#pragma unroll
+                                            for (int p = 0; p < 8; p++) acc[w][O][p] = __builtin_amdgcn_bitop3_b32(acc[w][O][p], y[w][p], y2[w][p], 0x96);
+                                    } else if (two == 1u) {
+#pragma unroll
+                                        for (int w = 0; w < 2; w++)
+#pragma unroll
+                                            for (int p = 0; p < 8; p++) acc[w][O][p] ^= y[w][p];
+                                    } else if (two == 2u) {
+#pragma unroll
+                                        for (int w = 0; w < 2; w++)
+#pragma unroll
+                                            for (int p = 0; p < 8; p++) acc[w][O][p] ^= y2[w][p];
+                                    }
+                                }
+                            });
+                            if (g < 3) {
+#pragma unroll
+                                for (int w = 0; w < 2; w++) mul2_planes(y2[w], y[w]);
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int w = 0; w < 2; w++) store_rows<OPW, true>(a, segs[w], c[w], rbase, cnt, acc[w]);
+    }
+}
+
+static uint8_t gmul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
+
+int main() {
+    const int k = 29, n = 80, ess = 256, nstripes = 9040, nseg = 8;
+    const int64_t spad = (int64_t)nstripes * k * ess, plen = (int64_t)nstripes * ess;
+    uint8_t *pieces, *out;
+    CK(hipMalloc(&pieces, plen * n * nseg));
+    CK(hipMalloc(&out, spad * nseg));
+    std::vector<uint8_t> h(plen * n * nseg);
+    for (auto &x : h) x = rand();
+    CK(hipMemcpy(pieces, h.data(), h.size(), hipMemcpyHostToDevice));
+    int cus = 0; CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    std::vector<std::vector<int>> sets;
+    { std::vector<int> s; for (int i = 51; i < 80; i++) s.push_back(i); sets.push_back(s); }
+    { std::mt19937 rng(29); std::vector<int> all(n); for (int i = 0; i < n; i++) all[i] = i;
+      std::shuffle(all.begin(), all.end(), rng); std::vector<int> s(all.begin(), all.begin() + k); std::sort(s.begin(), s.end()); sets.push_back(s); }
+    for (auto &ids : sets) {
+        // decode matrix for sorted ids (all < n); present data pass through
+        std::vector<uint8_t> m((size_t)k * k, 0);
+        for (int i = 0; i < k; i++) for (int j = 0; j < k; j++) m[i * k + j] = gen_entry(k, ids[i], j);
+        gf_invert(m.data(), k);
+        std::vector<int> missing; std::vector<bool> present(k, false);
+        for (int i : ids) if (i < k) present[i] = true;
+        for (int i = 0; i < k; i++) if (!present[i]) missing.push_back(i);
+        const int R = (int)missing.size();
+        const int ld = 32;
+        std::vector<uint8_t> coef((size_t)k * ld, 0);
+        for (int r = 0; r < R; r++) for (int c = 0; c < k; c++) coef[c * ld + r] = m[missing[r] * k + c];
+        uint8_t *dcoef; CK(hipMalloc(&dcoef, coef.size())); CK(hipMemcpy(dcoef, coef.data(), coef.size(), hipMemcpyHostToDevice));
+        RsArgs a{};
+        a.in_base = pieces; a.out_base = out; a.coef = dcoef; a.coef_ld = ld;
+        a.in_stripe_stride = ess; a.out_stripe_stride = (int64_t)k * ess;
+        a.in_seg_stride = plen * n; a.out_seg_stride = spad;
+        a.nin = k; a.nout = R;
+        for (int c = 0; c < k; c++) { a.in_off[c] = (int64_t)ids[c] * plen; a.copy_off[c] = ids[c] < k ? (int64_t)ids[c] * ess : -1; }
+        for (int r = 0; r < R; r++) a.out_off[r] = (int64_t)missing[r] * ess;
+        a.ess = ess; a.cps = ess / 16; a.nstripes = nstripes;
+        a.chunks_per_seg = (int64_t)nstripes * (ess / 16);
+        a.tiles_per_seg = (a.chunks_per_seg + 127) / 128;
+        a.total_tiles = a.tiles_per_seg * nseg;
+        const double bytes = 2.0 * spad * nseg;
+        // host reference for the first 64 columns of segment 0, stripe 0 (all rows)
+        std::vector<uint8_t> ref((size_t)k * ess);
+        for (int i = 0; i < k; i++) for (int t = 0; t < ess; t++) {
+            uint8_t acc = 0;
+            for (int c = 0; c < k; c++) acc ^= gmul(m[i * k + c], h[(size_t)ids[c] * plen + t]);
+            ref[i * ess + t] = acc;
+        }
+        auto timeit = [&](const char *name, auto launch) {
+            CK(hipMemset(out, 0, spad));
+            launch();
+            CK(hipDeviceSynchronize());
+            std::vector<uint8_t> got((size_t)k * ess);
+            CK(hipMemcpy(got.data(), out, got.size(), hipMemcpyDeviceToHost));
+            const bool ok = got == ref;
+            for (int i = 0; i < 2; i++) launch();
+            CK(hipDeviceSynchronize());
+            const int it = 10;
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < it; i++) launch();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = ms * 1e3 / it;
+            printf("m=%2d %-30s %8.1f us/8seg %7.1f us/seg %6.2f TB/s %s\n", R, name, us, us / nseg, bytes / us / 1e6, ok ? "ok" : "WRONG");
+            fflush(stdout);
+        };
+        {
+            const int grid = cus * 4;
+            timeit("bitbranch JC16 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 2, 16>), dim3(grid), dim3(256), 0, 0, a); });
+        }
+        for (int g : {1, 2}) {
+            const int grid = cus * g;
+            char nm[64];
+            snprintf(nm, 64, "two-tile bits JC16 grid%dx", g);
+            timeit(nm, [&] { hipLaunchKernelGGL((dec_two<8, 16, 0>), dim3(grid), dim3(256), 0, 0, a); });
+            snprintf(nm, 64, "two-tile pairs JC16 grid%dx", g);
+            timeit(nm, [&] { hipLaunchKernelGGL((dec_two<8, 16, 1>), dim3(grid), dim3(256), 0, 0, a); });
+            snprintf(nm, 64, "two-tile bits JC8 grid%dx", g);
+            timeit(nm, [&] { hipLaunchKernelGGL((dec_two<8, 8, 0>), dim3(grid), dim3(256), 0, 0, a); });
+        }
+        CK(hipFree(dcoef));
+    }
+    return 0;
+}

@@ -31,284 +31,98 @@
 //    and the rebuild matrix (G_S)^-1 of a share set).  The input's multiples
 //    x*2^b are formed once per input (21 XORs); each coefficient bit pair is
 //    then a wave-uniform branch adding one or two of them.
-#include <utility>
-
-#include "gf256.hpp"
-#include "rs_kernels.hpp"
+#include "rs_device.hpp"
 
 namespace uplink_ec {
 namespace {
 
-template <typename F, int... I>
-__device__ __forceinline__ void sf_impl(F &&f, std::integer_sequence<int, I...>) {
-    (f.template operator()<I>(), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-    sf_impl(f, std::make_integer_sequence<int, N>{});
-}
+using namespace dev;
 
 __constant__ GfTables d_gf = make_gf_tables();
 
-constexpr int kTileChunks = 128;  // 16-byte chunks per tile = 2048 byte columns
+// Warp-specialised tile pipeline shared by both kernels: waves 0..3 compute
+// output rows, waves 4..7 ("loaders") fetch the next work item's input
+// chunks (non-temporal 16-B loads), write the systematic copies, bit-slice
+// them and fill the other slot of a 2-slot LDS ring.  One LDS-only barrier
+// per item, so loads of item i+1 and the stores of item i overlap the XOR
+// work of item i and nothing waits for store completion.
+constexpr int kNC = 4;  // compute waves
+constexpr int kNL = 4;  // loader waves
+constexpr int kThreads = (kNC + kNL) * 64;
 
-__device__ __forceinline__ void swapmove(uint32_t &a, uint32_t &b, int s, uint32_t m) {
-    const uint32_t t = ((a >> s) ^ b) & m;
-    b ^= t;
-    a ^= t << s;
-}
-
-// 32 bytes (byte b of word w) -> 8 planes: plane p, bit 8b+w = bit p of byte (w,b).
-__device__ __forceinline__ void bitslice8(uint32_t (&w)[8]) {
-    swapmove(w[0], w[4], 4, 0x0F0F0F0Fu);
-    swapmove(w[1], w[5], 4, 0x0F0F0F0Fu);
-    swapmove(w[2], w[6], 4, 0x0F0F0F0Fu);
-    swapmove(w[3], w[7], 4, 0x0F0F0F0Fu);
-    swapmove(w[0], w[2], 2, 0x33333333u);
-    swapmove(w[1], w[3], 2, 0x33333333u);
-    swapmove(w[4], w[6], 2, 0x33333333u);
-    swapmove(w[5], w[7], 2, 0x33333333u);
-    swapmove(w[0], w[1], 1, 0x55555555u);
-    swapmove(w[2], w[3], 1, 0x55555555u);
-    swapmove(w[4], w[5], 1, 0x55555555u);
-    swapmove(w[6], w[7], 1, 0x55555555u);
-}
-
-// inverse of bitslice8 (each swap-move is an involution; reverse the stages)
-__device__ __forceinline__ void unbitslice8(uint32_t (&w)[8]) {
-    swapmove(w[0], w[1], 1, 0x55555555u);
-    swapmove(w[2], w[3], 1, 0x55555555u);
-    swapmove(w[4], w[5], 1, 0x55555555u);
-    swapmove(w[6], w[7], 1, 0x55555555u);
-    swapmove(w[0], w[2], 2, 0x33333333u);
-    swapmove(w[1], w[3], 2, 0x33333333u);
-    swapmove(w[4], w[6], 2, 0x33333333u);
-    swapmove(w[5], w[7], 2, 0x33333333u);
-    swapmove(w[0], w[4], 4, 0x0F0F0F0Fu);
-    swapmove(w[1], w[5], 4, 0x0F0F0F0Fu);
-    swapmove(w[2], w[6], 4, 0x0F0F0F0Fu);
-    swapmove(w[3], w[7], 4, 0x0F0F0F0Fu);
-}
-
-struct TileCols {
-    bool vA, vB;
-    int64_t inA, inB;    // byte offsets of the two chunks in an input share
-    int64_t outA, outB;  // byte offsets of the two chunks in an output row
-};
-
-__device__ __forceinline__ TileCols tile_cols(const RsArgs &a, int64_t tt, int lane) {
-    TileCols c;
-    const int64_t qA = tt * kTileChunks + lane;
-    const int64_t qB = qA + 64;
-    c.vA = qA < a.chunks_per_seg;
-    c.vB = qB < a.chunks_per_seg;
-    const uint32_t cps = (uint32_t)a.cps;
-    const uint32_t sA = (uint32_t)qA / cps, tA = (uint32_t)qA - sA * cps;
-    const uint32_t sB = (uint32_t)qB / cps, tB = (uint32_t)qB - sB * cps;
-    c.inA = (int64_t)sA * a.in_stripe_stride + (int64_t)tA * 16;
-    c.inB = (int64_t)sB * a.in_stripe_stride + (int64_t)tB * 16;
-    c.outA = (int64_t)sA * a.out_stripe_stride + (int64_t)tA * 16;
-    c.outB = (int64_t)sB * a.out_stripe_stride + (int64_t)tB * 16;
-    return c;
-}
-
-// Phase A: inputs j0 .. j0+jn-1 (thread handles j = j0 + wave + NW*i), load
-// two 16-byte chunks, optionally copy them through (systematic shares),
-// bit-slice and write the planes to lds[(j-j0)*8 + p][lane].
-template <int NW, int PER>
-__device__ __forceinline__ void stage_inputs(const RsArgs &a, int64_t seg, const TileCols &c, uint32_t *lds,
-                                             int lane, int wave, int j0, int jn, bool do_copy) {
-    uint4 bufA[PER], bufB[PER];
-    const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const int j = wave + NW * i;
-        if (j < jn) {
-            const uint8_t *p = in_seg + a.in_off[j0 + j];
-            bufA[i] = c.vA ? *(const uint4 *)(p + c.inA) : z;
-            bufB[i] = c.vB ? *(const uint4 *)(p + c.inB) : z;
-        }
-    }
-    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const int j = wave + NW * i;
-        if (j < jn) {
-            const int64_t co = a.copy_off[j0 + j];
-            if (do_copy && co >= 0) {
-                uint8_t *p = out_seg + co;
-                if (c.vA) *(uint4 *)(p + c.outA) = bufA[i];
-                if (c.vB) *(uint4 *)(p + c.outB) = bufB[i];
-            }
-            uint32_t w[8] = {bufA[i].x, bufA[i].y, bufA[i].z, bufA[i].w,
-                             bufB[i].x, bufB[i].y, bufB[i].z, bufB[i].w};
-            bitslice8(w);
-            uint32_t *dst = lds + j * 8 * 64 + lane;
-#pragma unroll
-            for (int p = 0; p < 8; p++) dst[p * 64] = w[p];
-        }
-    }
-}
-
-// Output: un-bit-slice each accumulated row and store its two chunks.
-template <int OPW>
-__device__ __forceinline__ void store_rows(const RsArgs &a, int64_t seg, const TileCols &c, int rbase, int cnt,
-                                           uint32_t (&acc)[OPW][8]) {
-    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
-    static_for<OPW>([&]<int O>() {
-        if (O < cnt) {
-            uint32_t w[8];
-#pragma unroll
-            for (int p = 0; p < 8; p++) w[p] = acc[O][p];
-            unbitslice8(w);
-            uint8_t *p = out_seg + a.out_off[rbase + O];
-            if (c.vA) *(uint4 *)(p + c.outA) = make_uint4(w[0], w[1], w[2], w[3]);
-            if (c.vB) *(uint4 *)(p + c.outB) = make_uint4(w[4], w[5], w[6], w[7]);
-        }
-    });
-}
-
-// ------------------------------------------------ compile-time-G encoder body
-template <int K, int N, int OPW, int W>
-__device__ __forceinline__ void compute_special(const uint32_t *lds, int lane, uint32_t (&acc)[OPW][8]) {
-    static_for<K>([&]<int J>() {
-        uint32_t x[8];
-        static_for<8>([&]<int P>() { x[P] = lds[(J * 8 + P) * 64 + lane]; });
-        uint32_t lo[16], hi[16];
-        lo[0] = 0;
-        hi[0] = 0;
-        static_for<15>([&]<int M1>() {
-            constexpr int M = M1 + 1;
-            constexpr int low = M & (-M);
-            constexpr int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
-            if constexpr (M == low) {
-                lo[M] = x[bit];
-                hi[M] = x[4 + bit];
-            } else {
-                lo[M] = lo[M ^ low] ^ x[bit];
-                hi[M] = hi[M ^ low] ^ x[4 + bit];
-            }
-        });
-        static_for<OPW>([&]<int O>() {
-            constexpr int r = W * OPW + O;
-            if constexpr (r < N - K) {
-                constexpr uint8_t cval = gen_entry(K, K + r, J);
-                static_for<8>([&]<int P>() {
-                    constexpr uint8_t row = mul_bitrow(cval, P);
-                    constexpr int L = row & 15, H = row >> 4;
-                    if constexpr (L != 0 && H != 0)
-                        acc[O][P] = __builtin_amdgcn_bitop3_b32(acc[O][P], lo[L], hi[H], 0x96);
-                    else if constexpr (L != 0)
-                        acc[O][P] ^= lo[L];
-                    else if constexpr (H != 0)
-                        acc[O][P] ^= hi[H];
-                });
-            }
-        });
-    });
-}
-
-template <int K, int N, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void rs_encode_special(const RsArgs a) {
+template <int K, int N>
+__global__ __launch_bounds__(kThreads, 1) void rs_encode_special(const RsArgs a) {
     constexpr int R = N - K;
-    constexpr int OPW = (R + NW - 1) / NW;
-    constexpr int PER = (K + NW - 1) / NW;
-    __shared__ uint32_t lds[K * 8 * 64];
+    constexpr int OPW = (R + kNC - 1) / kNC;
+    constexpr int PER = (K + kNL - 1) / kNL;
+    __shared__ uint32_t lds[2][K * 8 * 64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+    const bool loader = wave >= kNC;
+    const int lw = wave - kNC;
+    int64_t tile = blockIdx.x;
+    if (loader && tile < a.total_tiles) {
         const int64_t seg = tile / a.tiles_per_seg;
-        const int64_t tt = tile - seg * a.tiles_per_seg;
-        const TileCols c = tile_cols(a, tt, lane);
-        stage_inputs<NW, PER>(a, seg, c, lds, lane, wave, 0, K, true);
-        __syncthreads();
-        uint32_t acc[OPW][8];
-#pragma unroll
-        for (int o = 0; o < OPW; o++)
-#pragma unroll
-            for (int p = 0; p < 8; p++) acc[o][p] = 0;
-        static_for<NW>([&]<int W>() {
-            if (wave == W) compute_special<K, N, OPW, W>(lds, lane, acc);
-        });
-        const int rbase = wave * OPW;
-        const int cnt = R - rbase < OPW ? R - rbase : OPW;
-        store_rows<OPW>(a, seg, c, rbase, cnt, acc);
-        __syncthreads();
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        stage_inputs<kNL, PER, true>(a, seg, c, lds[0], lane, lw, 0, K, true);
     }
-}
-
-// ------------------------------------------------ runtime-matrix body
-__device__ __forceinline__ void mul2_planes(const uint32_t (&o)[8], uint32_t (&n)[8]) {
-    // v*2 mod 0x11d on bit planes: bit0 <- b7, bit1 <- b0, bit2 <- b1^b7,
-    // bit3 <- b2^b7, bit4 <- b3^b7, bit5 <- b4, bit6 <- b5, bit7 <- b6
-    n[0] = o[7];
-    n[1] = o[0];
-    n[2] = o[1] ^ o[7];
-    n[3] = o[2] ^ o[7];
-    n[4] = o[3] ^ o[7];
-    n[5] = o[4];
-    n[6] = o[5];
-    n[7] = o[6];
-}
-
-template <int OPW>
-__device__ __forceinline__ void compute_generic(const RsArgs &a, const uint32_t *lds, int lane, int jbase, int jn,
-                                                int rbase, int cnt, uint32_t (&acc)[OPW][8]) {
-    for (int jj = 0; jj < jn; jj++) {
-        uint32_t y[8][8];
+    lds_barrier();
+    int buf = 0;
+    for (; tile < a.total_tiles; tile += gridDim.x) {
+        if (loader) {
+            const int64_t next = tile + gridDim.x;
+            if (next < a.total_tiles) {
+                const int64_t seg = next / a.tiles_per_seg;
+                const TileCols c = tile_cols(a, next - seg * a.tiles_per_seg, lane);
+                stage_inputs<kNL, PER, true>(a, seg, c, lds[buf ^ 1], lane, lw, 0, K, true);
+            }
+        } else {
+            const int64_t seg = tile / a.tiles_per_seg;
+            const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+            uint32_t acc[OPW][8];
 #pragma unroll
-        for (int p = 0; p < 8; p++) y[0][p] = lds[(jj * 8 + p) * 64 + lane];
+            for (int o = 0; o < OPW; o++)
 #pragma unroll
-        for (int b = 1; b < 8; b++) mul2_planes(y[b - 1], y[b]);
-        const uint8_t *cp = a.coef + (int64_t)(jbase + jj) * a.coef_ld + rbase;
-        static_for<OPW / 4>([&]<int Q>() {
-            const uint32_t cw = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * Q));
-            static_for<4>([&]<int B>() {
-                constexpr int O = 4 * Q + B;
-                if (O < cnt) {
-                    const uint32_t cv = (cw >> (8 * B)) & 0xffu;
-                    static_for<4>([&]<int G2>() {
-                        const uint32_t two = (cv >> (2 * G2)) & 3u;
-                        if (two == 3u) {
-#pragma unroll
-                            for (int p = 0; p < 8; p++)
-                                acc[O][p] = __builtin_amdgcn_bitop3_b32(acc[O][p], y[2 * G2][p], y[2 * G2 + 1][p], 0x96);
-                        } else if (two == 1u) {
-#pragma unroll
-                            for (int p = 0; p < 8; p++) acc[O][p] ^= y[2 * G2][p];
-                        } else if (two == 2u) {
-#pragma unroll
-                            for (int p = 0; p < 8; p++) acc[O][p] ^= y[2 * G2 + 1][p];
-                        }
-                    });
-                }
+                for (int p = 0; p < 8; p++) acc[o][p] = 0;
+            static_for<kNC>([&]<int W>() {
+                if (wave == W) compute_special<K, N, OPW, W>(lds[buf], lane, acc);
             });
-        });
+            const int rbase = wave * OPW;
+            const int cnt = R - rbase < OPW ? R - rbase : OPW;
+            store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+        }
+        lds_barrier();
+        buf ^= 1;
     }
 }
 
+// Runtime-matrix kernel (rebuild, and encode for (k, n) without a
+// specialised kernel).  Compute-bound (the decode matrix is data), so all
+// four waves of a workgroup compute and four workgroups share a CU; inputs
+// are staged in LDS chunks of kGenericJC shares; each wave owns
+// ceil(nout / 4) rows (<= OPW) of a pass.
 constexpr int kGenericNW = 4;
-constexpr int kGenericJC = 16;  // inputs staged per LDS chunk
+constexpr int kGenericJC = 16;
 
 template <int OPW>
-__global__ __launch_bounds__(kGenericNW * 64) void rs_matmul_generic(const RsArgs a) {
+__global__ __launch_bounds__(kGenericNW * 64, 4) void rs_matmul_generic(const RsArgs a) {
     constexpr int NW = kGenericNW;
     constexpr int JC = kGenericJC;
-    constexpr int PER = (JC + NW - 1) / NW;
+    constexpr int PER = JC / NW;
     __shared__ uint32_t lds[JC * 8 * 64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int rows_per_pass = NW * OPW;
-    const int npass = (a.nout + rows_per_pass - 1) / rows_per_pass;
+    int per_wave = (a.nout + NW - 1) / NW;
+    per_wave = per_wave > OPW ? OPW : per_wave;
+    const int rows_per_pass = NW * per_wave;
+    const int npass = (a.nout > 0 && rows_per_pass > 0) ? (a.nout + rows_per_pass - 1) / rows_per_pass : 1;
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
-        const int64_t tt = tile - seg * a.tiles_per_seg;
-        const TileCols c = tile_cols(a, tt, lane);
-        for (int pass = 0; pass < (npass > 0 ? npass : 1); pass++) {
-            const int rbase = pass * rows_per_pass + wave * OPW;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        for (int pass = 0; pass < npass; pass++) {
+            const int rbase = pass * rows_per_pass + wave * per_wave;
             int cnt = a.nout - rbase;
-            cnt = cnt < 0 ? 0 : (cnt > OPW ? OPW : cnt);
+            cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
             uint32_t acc[OPW][8];
 #pragma unroll
             for (int o = 0; o < OPW; o++)
@@ -316,12 +130,12 @@ __global__ __launch_bounds__(kGenericNW * 64) void rs_matmul_generic(const RsArg
                 for (int p = 0; p < 8; p++) acc[o][p] = 0;
             for (int j0 = 0; j0 < a.nin; j0 += JC) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
-                stage_inputs<NW, PER>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
+                stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
                 __syncthreads();
                 if (cnt > 0) compute_generic<OPW>(a, lds, lane, j0, jn, rbase, cnt, acc);
                 __syncthreads();
             }
-            store_rows<OPW>(a, seg, c, rbase, cnt, acc);
+            store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
         }
     }
 }
@@ -380,10 +194,12 @@ int cu_count() {
     return g_cu_count;
 }
 
-template <int K, int N, int NW>
-hipError_t launch_special_nw(const RsArgs &a, int grid, hipStream_t s) {
-    if (grid <= 0) grid = default_grid(a.total_tiles, 2);
-    hipLaunchKernelGGL((rs_encode_special<K, N, NW>), dim3(grid), dim3(NW * 64), 0, s, a);
+template <int K, int N>
+hipError_t launch_special(const RsArgs &a, int grid, hipStream_t s) {
+    // LDS ring = 2 * K * 2 KiB; one workgroup per CU for K = 29, two for small K
+    const int per_cu = (2 * K * 2048) * 2 <= 160 * 1024 ? 2 : 1;
+    if (grid <= 0) grid = default_grid(a.total_tiles, per_cu);
+    hipLaunchKernelGGL((rs_encode_special<K, N>), dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 }  // namespace
@@ -399,9 +215,9 @@ bool have_special_encoder(int k, int n) {
 }
 
 hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStream_t s) {
-    if (k == 29 && n == 80) return launch_special_nw<29, 80, 4>(a, grid, s);
-    if (k == 20 && n == 60) return launch_special_nw<20, 60, 4>(a, grid, s);
-    if (k == 4 && n == 10) return launch_special_nw<4, 10, 4>(a, grid, s);
+    if (k == 29 && n == 80) return launch_special<29, 80>(a, grid, s);
+    if (k == 20 && n == 60) return launch_special<20, 60>(a, grid, s);
+    if (k == 4 && n == 10) return launch_special<4, 10>(a, grid, s);
     return hipErrorInvalidValue;
 }
 
