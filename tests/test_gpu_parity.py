@@ -1,0 +1,356 @@
+"""GPU parity: the HIP kernels behind include/uplink_ec.h against the oracle
+(CPU restatement of storj.io/infectious) and the golden fixtures.  Bit-exact
+is the only bar (byte-field arithmetic).  Mirrors the reference's test
+strategy: round trips over many (k, n, ess), fault tables,
+piece sizes, error strings, plus full-size BASELINE configurations."""
+import ctypes
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from uplink_amd import _native, eestream  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def scheme(k, n, ess):
+    return eestream.RSScheme(eestream.new_fec(k, n), ess)
+
+
+def gpu_encode(sch, seg: np.ndarray, nseg=1, parity_only=False):
+    k, n, ess = sch.fc.k, sch.fc.n, sch.ess
+    stripes = seg.size // (nseg * k * ess)
+    d_seg = torch.from_numpy(seg).cuda()
+    rows = n - k if parity_only else n
+    d_pieces = torch.full((nseg, rows, stripes * ess), 0xAB, dtype=torch.uint8, device="cuda")
+    eestream.SegmentCodec(sch).encode_segments(d_seg, nseg, stripes, d_pieces, parity_only=parity_only)
+    torch.cuda.synchronize()
+    return d_pieces
+
+
+def gpu_rebuild(sch, d_pieces, nums, stripes, nseg=1):
+    k, n, ess = sch.fc.k, sch.fc.n, sch.ess
+    plen = stripes * ess
+    rows = d_pieces.shape[1]
+    base = d_pieces.data_ptr()
+    out = torch.full((nseg, stripes * k * ess), 0xCD, dtype=torch.uint8, device="cuda")
+    eestream.SegmentCodec(sch).rebuild_segments(nums, [base + i * plen for i in nums], stripes, out, nseg=nseg,
+                                                piece_seg_stride=rows * plen, out_seg_stride=stripes * k * ess)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def test_golden_fixtures_on_gpu():
+    with open(os.path.join(HERE, "golden", "manifest.json")) as fh:
+        man = json.load(fh)
+    for case in man["cases"]:
+        z = np.load(os.path.join(HERE, "golden", case["file"]))
+        k, n, ess, stripes = case["k"], case["n"], case["ess"], case["stripes"]
+        sch = scheme(k, n, ess)
+        assert np.array_equal(sch.generator(), z["generator"])
+        d_pieces = gpu_encode(sch, z["segment"])
+        assert np.array_equal(d_pieces.cpu().numpy()[0], z["pieces"]), case["file"]
+        for nums in (list(range(n - k, n)), sorted(np.random.default_rng(7).choice(n, k, replace=False).tolist())):
+            assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], z["segment"])
+
+
+CONFIGS = [  # (k, n, ess, stripes): reference test configs + BASELINE shapes + edge cases
+    (1, 1, 64, 5), (1, 2, 64, 3), (2, 4, 1024, 3), (3, 7, 1024, 4), (4, 10, 256, 1025), (10, 20, 1024, 10),
+    (20, 60, 4096, 3), (29, 80, 256, 100), (30, 60, 1024, 7), (50, 80, 256, 3), (20, 50, 8192, 2),
+    (2, 4, 8, 5),        # ess < 16: byte kernel
+    (3, 5, 100, 4),      # ess not a multiple of 16: byte kernel
+    (7, 200, 256, 2),    # 193 parity rows: split over launches
+    (29, 80, 256, 1),    # a single stripe (tile tail)
+    (29, 80, 256, 129),  # ragged tile count
+]
+
+
+@pytest.mark.parametrize("k,n,ess,stripes", CONFIGS)
+def test_encode_rebuild_vs_oracle(oracle, k, n, ess, stripes):
+    rng = np.random.default_rng(k * 1000 + n + ess)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=4)
+    d_pieces = gpu_encode(sch, seg)
+    got = d_pieces.cpu().numpy()[0]
+    bad = np.nonzero((got != ref).any(axis=1))[0]
+    assert len(bad) == 0, f"pieces differ: {bad[:8]}"
+    sets = [list(range(n - k, n)), sorted(rng.choice(n, k, replace=False).tolist()), list(range(k))]
+    for nums in sets:
+        assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), nums
+
+
+def test_full_size_rs_29_80_64mib(oracle):
+    """BASELINE configs[1]/[2]: RS(29,80), 64 MiB segment (PadReader-padded to
+    9040 stripes), encode bit-exact vs the oracle, decode from exactly 29."""
+    k, n, ess = 29, 80, 256
+    raw = np.random.default_rng(0x5EED0000).integers(0, 256, 64 * 2**20, dtype=np.uint8)
+    seg = oracle.pad(raw, k * ess)
+    assert seg.size == 9040 * k * ess
+    sch = scheme(k, n, ess)
+    d_pieces = gpu_encode(sch, seg)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=min(os.cpu_count() or 1, 16))
+    assert np.array_equal(d_pieces.cpu().numpy()[0], ref)
+    for nums in (list(range(51, 80)), sorted(np.random.default_rng(29).choice(80, 29, replace=False).tolist())):
+        out = gpu_rebuild(sch, d_pieces, nums, 9040)[0]
+        assert np.array_equal(out, seg)
+        assert eestream.unpad(out.tobytes()) == raw.tobytes()
+
+
+def test_full_size_rs_20_60_ess4096(oracle):
+    """BASELINE configs[4] shape: RS(20,60), 4 KiB shares, 64 MiB segment."""
+    k, n, ess = 20, 60, 4096
+    raw = np.random.default_rng(5).integers(0, 256, 64 * 2**20, dtype=np.uint8)
+    seg = oracle.pad(raw, k * ess)
+    sch = scheme(k, n, ess)
+    d_pieces = gpu_encode(sch, seg)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=min(os.cpu_count() or 1, 16))
+    assert np.array_equal(d_pieces.cpu().numpy()[0], ref)
+    out = gpu_rebuild(sch, d_pieces, list(range(40, 60)), seg.size // (k * ess))[0]
+    assert np.array_equal(out, seg)
+
+
+def test_batched_segments_and_parity_only(oracle):
+    k, n, ess, stripes, nseg = 29, 80, 256, 37, 3
+    rng = np.random.default_rng(11)
+    segs = rng.integers(0, 256, nseg * stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    d_pieces = gpu_encode(sch, segs, nseg=nseg)
+    d_par = gpu_encode(sch, segs, nseg=nseg, parity_only=True)
+    f = oracle.FEC(k, n)
+    for g in range(nseg):
+        ref = f.encode_segment(segs[g * stripes * k * ess:(g + 1) * stripes * k * ess], ess)
+        assert np.array_equal(d_pieces[g].cpu().numpy(), ref)
+        assert np.array_equal(d_par[g].cpu().numpy(), ref[k:])
+    nums = sorted(rng.choice(n, k, replace=False).tolist())
+    out = gpu_rebuild(sch, d_pieces, nums, stripes, nseg=nseg)
+    assert np.array_equal(out.reshape(-1), segs)
+
+
+def test_rebuild_share_choice_and_errors():
+    """infectious Rebuild semantics through the C-ABI: unsorted and > k shares,
+    data pass-through, NotEnoughShares, invalid share id."""
+    k, n, ess, stripes = 3, 7, 256, 5
+    seg = np.random.default_rng(2).integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    d_pieces = gpu_encode(sch, seg)
+    assert np.array_equal(gpu_rebuild(sch, d_pieces, [6, 2, 0, 4, 5], stripes)[0], seg)
+    with pytest.raises(eestream.NotEnoughShares):
+        gpu_rebuild(sch, d_pieces, [0, 1], stripes)
+    with pytest.raises(eestream.InfectiousError, match="invalid share id"):
+        gpu_rebuild(sch, d_pieces[:, :], [0, 1, 7], stripes)
+
+
+def test_unaligned_buffers_take_byte_path(oracle):
+    k, n, ess, stripes = 4, 10, 256, 9
+    seg = np.random.default_rng(3).integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    buf = torch.zeros(seg.size + 1, dtype=torch.uint8, device="cuda")
+    buf[1:] = torch.from_numpy(seg).cuda()
+    pieces = torch.zeros(n * stripes * ess + 3, dtype=torch.uint8, device="cuda")
+    lib = _native.load()
+    rc = lib.ec_encode_segments(sch.ctx, buf.data_ptr() + 1, 1, stripes, pieces.data_ptr() + 3, 0,
+                                torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = pieces.cpu().numpy()[3:].reshape(n, -1)
+    assert np.array_equal(got, oracle.FEC(k, n).encode_segment(seg, ess))
+
+
+# ------------------------------------------------------------ scheme surface
+def test_encode_single_and_encode_match_oracle(oracle):
+    for k, n, ess in [(2, 4, 8 * 1024), (29, 80, 256), (3, 7, 100), (1, 4, 64)]:
+        sch = scheme(k, n, ess)
+        f = oracle.FEC(k, n)
+        stripe = np.random.default_rng(k).integers(0, 256, k * ess, dtype=np.uint8)
+        out = np.zeros(ess, dtype=np.uint8)
+        for num in range(n):
+            sch.encode_single(stripe, out, num)
+            assert np.array_equal(out, f.encode_single(stripe, num)), (k, n, num)
+        got = {}
+        sch.encode(stripe, lambda num, data: got.__setitem__(num, data.copy()))
+        ref = f.encode(stripe)
+        assert sorted(got) == list(range(n))
+        for num in range(n):
+            assert np.array_equal(got[num], ref[num])
+
+
+def test_encode_single_error_strings():
+    # segmentupload/encode_test.go:53,63 with RS(required 1, total 4), ess 64
+    rs = eestream.new_redundancy_strategy_from_storj(1, 2, 3, 4, 64)
+    data = np.ones(rs.stripe_size(), dtype=np.uint8)
+    out = np.zeros(64, dtype=np.uint8)
+    with pytest.raises(eestream.InfectiousError) as e1:
+        rs.encode_single(data, out, -1)
+    assert str(e1.value) == "num must be non-negative"
+    with pytest.raises(eestream.InfectiousError) as e2:
+        rs.encode_single(data, out, rs.total_count())
+    assert str(e2.value) == "num must be less than 4"
+
+
+def test_encoded_reader():
+    """TestEncodedReader (segmentupload/encode_test.go:16-68)."""
+    import io
+    rs = eestream.new_redundancy_strategy_from_storj(1, 2, 3, 4, 64)
+    expected = bytes([1]) * rs.stripe_size()
+    pieces = []
+    for i in range(rs.total_count()):
+        r = eestream.new_encoded_reader(io.BytesIO(expected), rs, i)
+        pieces.append(eestream.Share(i, np.frombuffer(r.read(), dtype=np.uint8)))
+    assert rs.decode(None, pieces).tobytes() == expected
+    r = eestream.new_encoded_reader(io.BytesIO(bytes([1]) * (rs.stripe_size() - 1)), rs, 0)
+    for _ in range(2):
+        with pytest.raises(EOFError, match="unexpected EOF"):
+            r.read()
+    for num, msg in [(-1, "num must be non-negative"), (rs.total_count(), "num must be less than 4")]:
+        r = eestream.new_encoded_reader(io.BytesIO(bytes([1]) * rs.stripe_size()), rs, num)
+        for _ in range(2):
+            with pytest.raises(eestream.InfectiousError) as ei:
+                r.read()
+            assert str(ei.value) == msg
+
+
+def _encode_pieces(rs, data: bytes):
+    import io
+    return [np.frombuffer(eestream.new_encoded_reader(io.BytesIO(data), rs, i).read(), dtype=np.uint8)
+            for i in range(rs.total_count())]
+
+
+def _decode_stream(rs, pieces: dict, nstripes: int, error_detection: bool):
+    """Stripe-by-stripe decode the way StripeReader.ReadStripes drives the
+    scheme (stripe.go:382-428): Rebuild, or Decode with error detection."""
+    ess, k = rs.erasure_share_size(), rs.required_count()
+    out = bytearray()
+    for s in range(nstripes):
+        shares = [eestream.Share(num, np.array(p[s * ess:(s + 1) * ess])) for num, p in sorted(pieces.items())]
+        if error_detection:
+            out += rs.decode(None, shares).tobytes()
+        else:
+            buf = bytearray(k * ess)
+
+            def put(sh):
+                buf[sh.number * ess:(sh.number + 1) * ess] = sh.data.tobytes()
+            rs.rebuild(shares, put)
+            out += buf
+    return bytes(out)
+
+
+def test_rs_roundtrip_like_testrs():
+    """TestRS (rs_test.go:32-60): RS(2,4), ess 8 KiB, 32 KiB."""
+    rs = eestream.RedundancyStrategy(scheme(2, 4, 8 * 1024), 0, 0)
+    data = os.urandom(32 * 1024)
+    pieces = _encode_pieces(rs, data)
+    assert _decode_stream(rs, dict(enumerate(pieces)), 2, False) == data
+
+
+# the fault tables of rs_test.go:194-342 at the scheme level: pieces that
+# error / EOF are missing; random-data pieces are corrupt (error detection)
+FAULT_TABLE = [  # (dataSize, blockSize, required, total, problematic)
+    (4 * 1024, 1024, 1, 1, 0), (4 * 1024, 1024, 1, 2, 0), (4 * 1024, 1024, 1, 2, 1), (4 * 1024, 1024, 2, 4, 0),
+    (4 * 1024, 1024, 2, 4, 1), (4 * 1024, 1024, 2, 4, 2), (6 * 1024, 1024, 3, 7, 0), (6 * 1024, 1024, 3, 7, 1),
+    (6 * 1024, 1024, 3, 7, 2), (6 * 1024, 1024, 3, 7, 3), (6 * 1024, 1024, 3, 7, 4),
+    (4 * 1024, 1024, 1, 1, 1), (4 * 1024, 1024, 1, 2, 2), (4 * 1024, 1024, 2, 4, 3), (6 * 1024, 1024, 3, 7, 5),
+]
+
+
+@pytest.mark.parametrize("size,ess,k,n,problematic", FAULT_TABLE)
+def test_missing_pieces_table(size, ess, k, n, problematic):
+    """TestRSErrors / TestRSEOF: the first `problematic` pieces are
+    unavailable; decoding works iff at least k remain."""
+    rs = eestream.RedundancyStrategy(scheme(k, n, ess), 0, 0)
+    data = os.urandom(size)
+    pieces = _encode_pieces(rs, data)
+    avail = {i: pieces[i] for i in range(problematic, n)}
+    nstripes = size // (k * ess)
+    if len(avail) < k:
+        with pytest.raises(eestream.NotEnoughShares):
+            _decode_stream(rs, avail, nstripes, False)
+    else:
+        assert _decode_stream(rs, avail, nstripes, False) == data
+
+
+@pytest.mark.parametrize("size,ess,k,n,problematic,fail", [
+    # TestRSRandomData (rs_test.go:317-342) with errorDetection=true and all pieces offered
+    (4 * 1024, 1024, 2, 4, 0, False), (4 * 1024, 1024, 2, 4, 1, False), (4 * 1024, 1024, 2, 4, 2, True),
+    (6 * 1024, 1024, 3, 7, 0, False), (6 * 1024, 1024, 3, 7, 1, False), (6 * 1024, 1024, 3, 7, 2, False),
+    (6 * 1024, 1024, 3, 7, 4, True), (4 * 1024, 1024, 1, 2, 1, True),
+])
+def test_random_data_pieces_error_detection(size, ess, k, n, problematic, fail):
+    rs = eestream.RedundancyStrategy(scheme(k, n, ess), 0, 0)
+    data = os.urandom(size)
+    pieces = _encode_pieces(rs, data)
+    rng = np.random.default_rng(problematic)
+    avail = {i: (rng.integers(0, 256, len(pieces[i]), dtype=np.uint8) if i < problematic else pieces[i])
+             for i in range(n)}
+    nstripes = size // (k * ess)
+    if fail:
+        try:
+            got = _decode_stream(rs, avail, nstripes, True)
+        except (eestream.NotEnoughShares, eestream.TooManyErrors):
+            return
+        assert got != data
+    else:
+        assert _decode_stream(rs, avail, nstripes, True) == data
+
+
+def test_decode_corrects_scattered_errors_rs_29_80(oracle):
+    k, n, ess = 29, 80, 256
+    sch = scheme(k, n, ess)
+    rng = np.random.default_rng(8)
+    stripe = rng.integers(0, 256, k * ess, dtype=np.uint8)
+    allsh = oracle.FEC(k, n).encode(stripe)
+    nums = sorted(rng.choice(n, 45, replace=False).tolist())  # e = 8
+    shares = [eestream.Share(i, np.array(allsh[i])) for i in nums]
+    for i in rng.choice(45, 8, replace=False):
+        shares[i].data[rng.integers(0, ess, 20)] ^= rng.integers(1, 256, 20, dtype=np.uint8)
+    got = sch.decode(None, shares)
+    assert np.array_equal(got, stripe)
+    # Decode corrects the shares in place (infectious semantics)
+    for s in shares:
+        assert np.array_equal(s.data, allsh[s.number])
+
+
+def test_calc_piece_size_matches_encoded_reader():
+    rs = eestream.RedundancyStrategy(scheme(2, 4, 1024), 0, 0)
+    import io
+    for size in (0, 1, 1020, 1024, 32764, 32768, 32868):
+        padded = eestream.pad(os.urandom(size), rs.stripe_size())
+        for i in range(rs.total_count()):
+            piece = eestream.new_encoded_reader(io.BytesIO(padded), rs, i).read()
+            assert len(piece) == eestream.calc_piece_size(size, rs)
+
+
+def test_concurrent_encode_single(oracle):
+    """EncodeSingle is called from many goroutines at once (uplink.go:83)."""
+    k, n, ess = 29, 80, 256
+    sch = scheme(k, n, ess)
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(12)
+    stripes = [rng.integers(0, 256, k * ess, dtype=np.uint8) for _ in range(6)]
+    errors = []
+
+    def work(t):
+        out = np.zeros(ess, dtype=np.uint8)
+        for rep in range(10):
+            s = stripes[(t + rep) % len(stripes)]
+            num = (t * 7 + rep * 13) % n
+            sch.encode_single(s, out, num)
+            if not np.array_equal(out, f.encode_single(s, num)):
+                errors.append((t, rep))
+    th = [threading.Thread(target=work, args=(t,)) for t in range(12)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors

@@ -1,0 +1,187 @@
+"""Pin the oracle (CPU restatement of storj.io/infectious v0.0.2) before
+trusting it.  The reference's own tests pin round trips, piece sizes and error
+strings but no parity byte; the generator is therefore checked
+two independent ways plus the SURVEY Appendix A fingerprints."""
+import hashlib
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import infectious_np as NP
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_gf_exp_prefix():
+    # gf_exp begins 1,2,4,...,38 (poly 0x11d, alpha 2)
+    assert NP.EXP[:16].tolist() == [1, 2, 4, 8, 16, 32, 64, 128, 29, 58, 116, 232, 205, 135, 19, 38]
+    for a in range(1, 256):
+        assert NP.MUL[a, NP.INV[a]] == 1
+
+
+FINGERPRINTS = {  # (row k prefix, row n-1 prefix, sum of all entries)
+    (2, 4): ([3, 2], [5, 4], 16),
+    (4, 10): ([119, 64, 56, 14], [27, 22, 113, 125], 2370),
+    (29, 80): ([248, 170, 37, 161, 205, 84, 235, 155], [219, 125, 201, 16, 150, 85, 10, 31], 192414),
+    (20, 60): ([183, 174, 11, 114, 11, 205, 41, 63], [21, 141, 191, 62, 127, 62, 207, 154], 106026),
+}
+
+
+@pytest.mark.parametrize("kn", sorted(FINGERPRINTS))
+def test_generator_fingerprints(oracle, kn):
+    k, n = kn
+    G, _ = oracle.new_fec(k, n)
+    rk, rn, total = FINGERPRINTS[kn]
+    assert G[k, :len(rk)].tolist() == rk
+    assert G[n - 1, :len(rn)].tolist() == rn
+    assert int(G.astype(np.int64).sum()) == total
+
+
+@pytest.mark.parametrize("kn", [(1, 1), (1, 4), (2, 4), (3, 7), (4, 10), (10, 20), (20, 60), (29, 80), (30, 60),
+                                (50, 80), (10, 256), (256, 256), (128, 200)])
+def test_generator_constructions_agree(oracle, kn):
+    """zfec inverted-Vandermonde (C oracle) == closed-form Lagrange (C) ==
+    numpy Lagrange restatement; systematic top block."""
+    k, n = kn
+    G, _ = oracle.new_fec(k, n)
+    assert np.array_equal(G, oracle.lagrange_fec(k, n))
+    if n * k <= 4000:
+        assert np.array_equal(G, NP.new_fec(k, n))
+    assert np.array_equal(G[:k], np.eye(k, dtype=np.uint8))
+    if k == 1:
+        assert (G == 1).all()  # RS(1, n) is replication
+
+
+def test_new_fec_param_errors(oracle):
+    for k, n in [(0, 1), (2, 1), (1, 257), (-1, 4), (3, 0)]:
+        with pytest.raises(ValueError, match="requires 1 <= k <= n <= 256"):
+            oracle.new_fec(k, n)
+
+
+@pytest.mark.parametrize("kn", [(3, 7), (4, 10), (2, 4), (1, 3)])
+def test_mds_every_k_subset_rebuilds(oracle, kn):
+    k, n = kn
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(1)
+    data = rng.integers(0, 256, k * 64, dtype=np.uint8)
+    shares = f.encode(data)
+    for sub in itertools.combinations(range(n), k):
+        got = f.rebuild(list(sub), [shares[i] for i in sub])
+        assert np.array_equal(got.reshape(-1), data), sub
+
+
+def test_encode_single_errors_pinned(oracle):
+    # segmentupload/encode_test.go:53,63 pin these two strings (RS total 4)
+    f = oracle.FEC(1, 4)
+    stripe = np.ones(64, dtype=np.uint8)
+    with pytest.raises(oracle.OracleError, match="^num must be non-negative$"):
+        f.encode_single(stripe, -1)
+    with pytest.raises(oracle.OracleError, match="^num must be less than 4$"):
+        f.encode_single(stripe, 4)
+
+
+def test_encode_single_matches_encode(oracle):
+    f = oracle.FEC(5, 9)
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 5 * 33, dtype=np.uint8)
+    allsh = f.encode(data)
+    for num in range(9):
+        assert np.array_equal(f.encode_single(data, num), allsh[num])
+        assert np.array_equal(NP.encode_single(f.enc, data, num), allsh[num])
+
+
+def test_numpy_and_c_segment_encode_agree(oracle):
+    k, n, ess, stripes = 4, 10, 64, 7
+    rng = np.random.default_rng(4)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    f = oracle.FEC(k, n)
+    assert np.array_equal(f.encode_segment(seg, ess), NP.encode_segment(f.enc, seg, ess))
+    for simd in (0, 1, 2):  # scalar / SSSE3 / AVX2 addmul give identical bytes
+        if simd > oracle.lib().or_get_simd():
+            continue
+        oracle.lib().or_set_simd(simd)
+        assert np.array_equal(f.encode_segment(seg, ess, threads=3), NP.encode_segment(f.enc, seg, ess))
+    oracle.lib().or_set_simd(-1)
+
+
+def test_rebuild_front_back_choice_and_errors(oracle):
+    """infectious Rebuild: sort by number, front share when its number == i,
+    else take from the back; fewer than k -> NotEnoughShares; number >= n ->
+    invalid share id."""
+    f = oracle.FEC(3, 7)
+    data = np.arange(3 * 16, dtype=np.uint8)
+    sh = f.encode(data)
+    # more than k shares, unsorted: data 0 and 2 present, 1 missing
+    nums = [6, 2, 0, 4, 5]
+    got = f.rebuild(nums, [sh[i] for i in nums])
+    assert np.array_equal(got.reshape(-1), data)
+    with pytest.raises(oracle.OracleError, match="not enough shares"):
+        f.rebuild([0, 1], [sh[0], sh[1]])
+    with pytest.raises(oracle.OracleError, match="invalid share id"):
+        f.rebuild([0, 1, 9], [sh[0], sh[1], sh[2]])
+
+
+def test_decode_corrects_errors_berlekamp_welch(oracle):
+    k, n = 3, 7
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, k * 40, dtype=np.uint8)
+    sh = f.encode(data)
+    # 7 shares, e = 2: two corrupted shares are corrected
+    bad = [np.array(s) for s in sh]
+    bad[1] = rng.integers(0, 256, 40, dtype=np.uint8)
+    bad[5] ^= 0x5A
+    assert np.array_equal(f.decode(list(range(n)), bad), data)
+    # k+1 shares with an error: e = 0 -> NotEnoughShares (stripe.go:419-424 retries with more)
+    b4 = [np.array(sh[i]) for i in range(4)]
+    b4[0] ^= 1
+    with pytest.raises(oracle.OracleError, match="not enough shares"):
+        f.decode([0, 1, 2, 3], b4)
+    # no errors with extra shares decodes
+    assert np.array_equal(f.decode([0, 2, 3, 6], [sh[i] for i in (0, 2, 3, 6)]), data)
+
+
+@pytest.mark.parametrize("size,expected", [
+    (0, 1024), (1, 1024), (1024 - 4, 1024), (1024, 1024),
+    (32 * 1024 - 4, 16384), (32 * 1024, 17408), (32 * 1024 + 100, 17408)])
+def test_calc_piece_size_pad_rule(oracle, size, expected):
+    """TestCalcPieceSize (rs_test.go:636-668): RS(2,4), ess 1 KiB; the piece
+    length after PadReader + EncodeReader equals CalcPieceSize."""
+    k, n, ess = 2, 4, 1024
+    data = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8)
+    padded = oracle.pad(data, k * ess)
+    assert len(padded) % (k * ess) == 0
+    assert bytes(padded) == NP.pad(data.tobytes(), k * ess)
+    pieces = oracle.FEC(k, n).encode_segment(padded, ess)
+    assert pieces.shape[1] == expected == NP.calc_piece_size(size, k, ess)
+    p = len(padded) - size
+    assert int.from_bytes(bytes(padded[-4:]), "big") == p
+    assert all(b == (p & 0xFF) for b in padded[size:-4])
+
+
+def test_golden_fixtures_reproduce(oracle):
+    with open(os.path.join(HERE, "golden", "manifest.json")) as fh:
+        man = json.load(fh)
+    for case in man["cases"]:
+        z = np.load(os.path.join(HERE, "golden", case["file"]))
+        f = oracle.FEC(case["k"], case["n"])
+        assert hashlib.sha256(f.enc.tobytes()).hexdigest() == case["generator_sha256"]
+        pieces = f.encode_segment(z["segment"], case["ess"])
+        assert np.array_equal(pieces, z["pieces"])
+        assert hashlib.sha256(pieces.tobytes()).hexdigest() == case["pieces_sha256"]
+        assert np.array_equal(NP.encode_segment(f.enc, z["segment"], case["ess"]), z["pieces"])
+
+
+def test_baseline_rebuild_matches(oracle):
+    k, n, ess = 29, 80, 256
+    f = oracle.FEC(k, n)
+    seg = np.random.default_rng(9).integers(0, 256, 6 * k * ess, dtype=np.uint8)
+    pieces = f.encode_segment(seg, ess, threads=4)
+    for nums in (list(range(51, 80)), sorted(np.random.default_rng(29).choice(80, 29, replace=False).tolist())):
+        out = f.rebuild_segment(nums, [pieces[i] for i in nums], ess, threads=3)
+        assert np.array_equal(out, seg)
+        out2 = NP.rebuild_segment(f.enc, nums, [pieces[i] for i in nums], ess)
+        assert np.array_equal(out2, seg)

@@ -224,8 +224,6 @@ class RSScheme:
         rc = self._lib.ec_decode(self._ctx, len(shares), nums, ptrs, ln, _ptr(tmp))
         if len(shares) >= k:
             self._resort(shares, nums, ptrs, datas)
-            for s, d in zip(shares, [x.data for x in shares]):
-                pass
         _raise(self._ctx, rc)
         dst[:] = tmp[:need]
         return dst
