@@ -24,6 +24,49 @@ __device__ __forceinline__ void body(const RsArgs &a, const uint32_t *lds, int l
         compute_generic<OPW>(a, lds, lane, jbase, jn, rbase, cnt, acc);
         return;
     }
+    if constexpr (MODE == 4) {
+        // bit branches + software prefetch of the next input's planes and coefficients
+        uint32_t yn[8];
+        uint32_t cwn[(OPW + 3) / 4];
+        const uint8_t *cp0 = a.coef + (int64_t)jbase * a.coef_ld + rbase;
+#pragma unroll
+        for (int p = 0; p < 8; p++) yn[p] = lds[p * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < (OPW + 3) / 4; q++) cwn[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp0 + 4 * q));
+        for (int jj = 0; jj < jn; jj++) {
+            uint32_t y[8];
+            uint32_t cw[(OPW + 3) / 4];
+#pragma unroll
+            for (int p = 0; p < 8; p++) y[p] = yn[p];
+#pragma unroll
+            for (int q = 0; q < (OPW + 3) / 4; q++) cw[q] = cwn[q];
+            if (jj + 1 < jn) {
+                const uint8_t *cp = a.coef + (int64_t)(jbase + jj + 1) * a.coef_ld + rbase;
+#pragma unroll
+                for (int p = 0; p < 8; p++) yn[p] = lds[((jj + 1) * 8 + p) * 64 + lane];
+#pragma unroll
+                for (int q = 0; q < (OPW + 3) / 4; q++) cwn[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * q));
+            }
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                static_for<OPW>([&]<int O>() {
+                    if (O < cnt) {
+                        if ((cw[O / 4] >> (8 * (O % 4) + b)) & 1u) {
+#pragma unroll
+                            for (int p = 0; p < 8; p++) acc[O][p] ^= y[p];
+                        }
+                    }
+                });
+                if (b < 7) {
+                    uint32_t n[8];
+                    mul2_planes(y, n);
+#pragma unroll
+                    for (int p = 0; p < 8; p++) y[p] = n[p];
+                }
+            }
+        }
+        return;
+    }
     for (int jj = 0; jj < jn; jj++) {
         uint32_t y[8][8];
 #pragma unroll
@@ -43,7 +86,13 @@ __device__ __forceinline__ void body(const RsArgs &a, const uint32_t *lds, int l
                             const uint32_t m = __builtin_amdgcn_readfirstlane(0u - ((cv >> b) & 1u));
 #pragma unroll
                             for (int p = 0; p < 8; p++)
-                                acc[O][p] = __builtin_amdgcn_bitop3_b32(acc[O][p], y[b][p], m, 0x6a);  // a ^ (b & c)
+                                acc[O][p] = __builtin_amdgcn_bitop3_b32(acc[O][p], y[b][p], m, 0x78);  // a ^ (b & c), LUT index = 4*S0 + 2*S1 + S2
+                        }
+                    } else if constexpr (MODE == 3) {
+#pragma unroll
+                        for (int b = 0; b < 8; b++) {
+#pragma unroll
+                            for (int p = 0; p < 8; p++) acc[O][p] ^= y[b][p];
                         }
                     } else {
 #pragma unroll
@@ -60,9 +109,8 @@ __device__ __forceinline__ void body(const RsArgs &a, const uint32_t *lds, int l
     }
 }
 
-template <int OPW, int MODE, int JC>
-__global__ __launch_bounds__(256, 2) void dec_plain(const RsArgs a) {
-    constexpr int NW = 4;
+template <int OPW, int MODE, int JC, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 2) void dec_plain(const RsArgs a) {
     constexpr int PER = JC / NW;
     __shared__ uint32_t lds[JC * 8 * 64];
     const int lane = threadIdx.x & 63;
@@ -209,9 +257,109 @@ __global__ __launch_bounds__(256, 2) void dec_two(const RsArgs a) {
     }
 }
 
+
+template <int OPW, int MODE>
+__device__ __forceinline__ void body2(const uint32_t *lds, const uint8_t *lcoef, int lane, int jn, int rbase_local,
+                                      int cnt, uint32_t (&acc)[OPW][8]) {
+    for (int jj = 0; jj < jn; jj++) {
+        uint32_t y[8];
+#pragma unroll
+        for (int p = 0; p < 8; p++) y[p] = lds[(jj * 8 + p) * 64 + lane];
+        uint32_t cv[OPW];
+#pragma unroll
+        for (int o = 0; o < OPW; o++) cv[o] = __builtin_amdgcn_readfirstlane((uint32_t)lcoef[jj * 64 + rbase_local + o]);
+        if constexpr (MODE == 5) {
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                static_for<OPW>([&]<int O>() {
+                    if (O < cnt) {
+                        if ((cv[O] >> b) & 1u) {
+#pragma unroll
+                            for (int p = 0; p < 8; p++) acc[O][p] ^= y[p];
+                        }
+                    }
+                });
+                if (b < 7) {
+                    uint32_t n[8];
+                    mul2_planes(y, n);
+#pragma unroll
+                    for (int p = 0; p < 8; p++) y[p] = n[p];
+                }
+            }
+        } else {
+            uint32_t m[8][8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) m[0][p] = y[p];
+#pragma unroll
+            for (int b = 1; b < 8; b++) mul2_planes(m[b - 1], m[b]);
+            static_for<OPW>([&]<int O>() {
+                if (O < cnt) {
+                    static_for<2>([&]<int H>() {
+                        const uint32_t nib = (cv[O] >> (4 * H)) & 15u;
+                        switch (nib) {
+#define NCASE(V)                                                                              \
+    case V:                                                                                   \
+        static_for<8>([&]<int P>() {                                                          \
+            uint32_t t = 0;                                                                   \
+            if constexpr ((V)&1) t ^= m[4 * H + 0][P];                                         \
+            if constexpr ((V)&2) t ^= m[4 * H + 1][P];                                         \
+            if constexpr ((V)&4) t ^= m[4 * H + 2][P];                                         \
+            if constexpr ((V)&8) t ^= m[4 * H + 3][P];                                         \
+            acc[O][P] ^= t;                                                                   \
+        });                                                                                   \
+        break;
+                            NCASE(1) NCASE(2) NCASE(3) NCASE(4) NCASE(5) NCASE(6) NCASE(7) NCASE(8)
+                            NCASE(9) NCASE(10) NCASE(11) NCASE(12) NCASE(13) NCASE(14) NCASE(15)
+#undef NCASE
+                            default: break;
+                        }
+                    });
+                }
+            });
+        }
+    }
+}
+
+template <int OPW, int MODE, int JC>
+__global__ __launch_bounds__(256, 2) void dec_lc(const RsArgs a) {
+    constexpr int NW = 4;
+    constexpr int PER = JC / NW;
+    __shared__ uint32_t lds[JC * 8 * 64];
+    __shared__ uint8_t lcoef[JC * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int per_wave = (a.nout + NW - 1) / NW;
+    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const int64_t seg = tile / a.tiles_per_seg;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        const int rbase = wave * per_wave;
+        int cnt = a.nout - rbase;
+        cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
+        uint32_t acc[OPW][8];
+#pragma unroll
+        for (int o = 0; o < OPW; o++)
+#pragma unroll
+            for (int p = 0; p < 8; p++) acc[o][p] = 0;
+        for (int j0 = 0; j0 < a.nin; j0 += JC) {
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            for (int i = threadIdx.x; i < JC * 64; i += NW * 64) {
+                const int jj = i >> 6, r = i & 63;
+                lcoef[i] = (jj < jn && r < a.nout) ? a.coef[(int64_t)(j0 + jj) * a.coef_ld + r] : 0;
+            }
+            stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, true);
+            __syncthreads();
+            if (cnt > 0) body2<OPW, MODE>(lds, lcoef, lane, jn, rbase, cnt, acc);
+            __syncthreads();
+        }
+        store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+    }
+}
+
 static uint8_t gmul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
 
-int main() {
+int main(int argc, char **argv) {
+    const int only = argc > 1 ? atoi(argv[1]) : -1;  // run one variant (for PMC passes)
+    int vidx = 0;
     const int k = 29, n = 80, ess = 256, nstripes = 9040, nseg = 8;
     const int64_t spad = (int64_t)nstripes * k * ess, plen = (int64_t)nstripes * ess;
     uint8_t *pieces, *out;
@@ -227,6 +375,7 @@ int main() {
     { std::mt19937 rng(29); std::vector<int> all(n); for (int i = 0; i < n; i++) all[i] = i;
       std::shuffle(all.begin(), all.end(), rng); std::vector<int> s(all.begin(), all.begin() + k); std::sort(s.begin(), s.end()); sets.push_back(s); }
     for (auto &ids : sets) {
+        vidx = 0;
         // decode matrix for sorted ids (all < n); present data pass through
         std::vector<uint8_t> m((size_t)k * k, 0);
         for (int i = 0; i < k; i++) for (int j = 0; j < k; j++) m[i * k + j] = gen_entry(k, ids[i], j);
@@ -238,6 +387,7 @@ int main() {
         const int ld = 32;
         std::vector<uint8_t> coef((size_t)k * ld, 0);
         for (int r = 0; r < R; r++) for (int c = 0; c < k; c++) coef[c * ld + r] = m[missing[r] * k + c];
+        coef.resize(coef.size() + 64, 0);
         uint8_t *dcoef; CK(hipMalloc(&dcoef, coef.size())); CK(hipMemcpy(dcoef, coef.data(), coef.size(), hipMemcpyHostToDevice));
         RsArgs a{};
         a.in_base = pieces; a.out_base = out; a.coef = dcoef; a.coef_ld = ld;
@@ -259,6 +409,7 @@ int main() {
             ref[i * ess + t] = acc;
         }
         auto timeit = [&](const char *name, auto launch) {
+            if (only >= 0 && vidx++ != only) return;
             CK(hipMemset(out, 0, spad));
             launch();
             CK(hipDeviceSynchronize());
@@ -279,17 +430,10 @@ int main() {
         };
         {
             const int grid = cus * 4;
-            timeit("bitbranch JC16 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 2, 16>), dim3(grid), dim3(256), 0, 0, a); });
-        }
-        for (int g : {1, 2}) {
-            const int grid = cus * g;
-            char nm[64];
-            snprintf(nm, 64, "two-tile bits JC16 grid%dx", g);
-            timeit(nm, [&] { hipLaunchKernelGGL((dec_two<8, 16, 0>), dim3(grid), dim3(256), 0, 0, a); });
-            snprintf(nm, 64, "two-tile pairs JC16 grid%dx", g);
-            timeit(nm, [&] { hipLaunchKernelGGL((dec_two<8, 16, 1>), dim3(grid), dim3(256), 0, 0, a); });
-            snprintf(nm, 64, "two-tile bits JC8 grid%dx", g);
-            timeit(nm, [&] { hipLaunchKernelGGL((dec_two<8, 8, 0>), dim3(grid), dim3(256), 0, 0, a); });
+            timeit("OLD bitbranch JC16 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 2, 16>), dim3(grid), dim3(256), 0, 0, a); });
+            timeit("LDS-coef bitbranch grid4x", [&] { hipLaunchKernelGGL((dec_lc<8, 5, 16>), dim3(grid), dim3(256), 0, 0, a); });
+            timeit("LDS-coef nibble-switch grid4x", [&] { hipLaunchKernelGGL((dec_lc<8, 6, 16>), dim3(grid), dim3(256), 0, 0, a); });
+            timeit("LDS-coef nibble-switch grid2x", [&] { hipLaunchKernelGGL((dec_lc<8, 6, 16>), dim3(cus * 2), dim3(256), 0, 0, a); });
         }
         CK(hipFree(dcoef));
     }

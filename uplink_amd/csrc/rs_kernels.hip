@@ -97,16 +97,16 @@ __global__ __launch_bounds__(kThreads, 1) void rs_encode_special(const RsArgs a)
 }
 
 // Runtime-matrix kernel (rebuild, and encode for (k, n) without a
-// specialised kernel).  Compute-bound (the decode matrix is data), so all
-// four waves of a workgroup compute and four workgroups share a CU; inputs
-// are staged in LDS chunks of kGenericJC shares; each wave owns
-// ceil(nout / 4) rows (<= OPW) of a pass.
-constexpr int kGenericNW = 4;
+// specialised kernel).  Compute-bound (the decode matrix is data), so every
+// wave computes (no loader waves) and four workgroups share a CU; inputs
+// are staged in LDS chunks of kGenericJC shares; each of the NW waves owns
+// ceil(nout / NW) rows (<= OPW) of a pass.  8 waves x 4 rows (77 VGPRs, 6
+// waves/SIMD) beat 4 waves x 8 rows for decode (69 vs 80 us per RS(29,80)
+// 64 MiB segment at m = 29, tools/exp/decode_exp.hip).
 constexpr int kGenericJC = 16;
 
-template <int OPW>
-__global__ __launch_bounds__(kGenericNW * 64, 4) void rs_matmul_generic(const RsArgs a) {
-    constexpr int NW = kGenericNW;
+template <int OPW, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) {
     constexpr int JC = kGenericJC;
     constexpr int PER = JC / NW;
     __shared__ uint32_t lds[JC * 8 * 64];
@@ -223,13 +223,12 @@ hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStr
 
 hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
     if (grid <= 0) grid = default_grid(a.total_tiles, 4);
-    const dim3 block(kGenericNW * 64);
-    if (a.nout <= kGenericNW * 4)
-        hipLaunchKernelGGL(rs_matmul_generic<4>, dim3(grid), block, 0, s, a);
-    else if (a.nout <= kGenericNW * 8)
-        hipLaunchKernelGGL(rs_matmul_generic<8>, dim3(grid), block, 0, s, a);
+    if (a.nout <= 8 * 4)
+        hipLaunchKernelGGL((rs_matmul_generic<4, 8>), dim3(grid), dim3(8 * 64), 0, s, a);
+    else if (a.nout <= 4 * 16)
+        hipLaunchKernelGGL((rs_matmul_generic<16, 4>), dim3(grid), dim3(4 * 64), 0, s, a);
     else
-        hipLaunchKernelGGL(rs_matmul_generic<16>, dim3(grid), block, 0, s, a);
+        hipLaunchKernelGGL((rs_matmul_generic<16, 8>), dim3(grid), dim3(8 * 64), 0, s, a);
     return hipGetLastError();
 }
 
