@@ -23,9 +23,12 @@
  *
  * Parity pinning: the reference's own tests pin round trips, piece sizes and
  * two error strings (rs_test.go, segmentupload/encode_test.go:53,63) but no
- * parity byte.  The generator matrix is therefore built two independent ways
- * here (the zfec inverted-Vandermonde construction and the closed-form
- * Lagrange basis) and the two must agree; see tests/test_oracle.py.
+ * parity byte, and no Go toolchain / infectious copy exists here to run.  The
+ * generator matrix is therefore built two independent ways here (the zfec
+ * inverted-Vandermonde construction and the closed-form Lagrange basis) and
+ * the two must agree, plus the SURVEY Appendix A fingerprints; see
+ * tests/test_oracle.py.  Exact parity bytes are therefore "parity unpinned"
+ * with respect to an execution of the reference.
  *
  * Reference-shaped CPU baseline helpers (or_baseline_*) reproduce the
  * per-piece, per-stripe EncodeSingle loop of segmentupload/encode.go:39-75 and
