@@ -25,6 +25,7 @@
  *                            by single.go:228-238 (pieceReader.PieceReader)
  *   ec_rebuild_segments      batch form of the per-stripe Rebuild loop of
  *                            StripeReader.ReadStripes  stripe.go:382-428
+ *   ec_*_segments_host       the same batches from/to host memory (PCIe pipeline)
  *   ec_strerror/ec_format_error  error texts of infectious / eestream
  *
  * Error codes map to the errors eestream's callers test:
@@ -119,6 +120,22 @@ int ec_rebuild_segments(const ec_ctx *ctx, int nshares, const int *nums, const u
 int ec_rebuild_segments_batched(const ec_ctx *ctx, int nshares, const int *nums, const uint8_t *const *pieces,
                                 size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
                                 uint8_t *out, ec_stream stream);
+
+/* ---- host-memory pipeline (end-to-end path, PCIe-inclusive) ----
+ * Same layouts as the device calls, but in host memory (pinned memory from
+ * ec_host_alloc gives full-speed DMA).  Segments are streamed through a ring
+ * of device slots on 3 HIP streams so H2D, kernel and D2H of consecutive
+ * segments overlap; synchronous (returns when every piece is in host memory).
+ * This is the form the Go side calls from segmentupload (SegmentEncoder,
+ * single.go:233-238) and StripeReader (BatchRebuilder, stripe.go:382-428). */
+int ec_encode_segments_host(const ec_ctx *ctx, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                            int flags);
+/* pieces[i]: host pointer of share nums[i] for segment 0; segment g's copy of
+ * that share is at pieces[i] + g*piece_seg_stride. out: [nseg][stripes*k*ess] */
+int ec_rebuild_segments_host(const ec_ctx *ctx, int nshares, const int *nums, const uint8_t *const *pieces,
+                             size_t nstripes, size_t nseg, long long piece_seg_stride, uint8_t *out);
+void *ec_host_alloc(size_t bytes); /* pinned (hipHostMalloc); NULL on failure */
+void ec_host_free(void *p);
 
 /* ---- device helpers ---- */
 int ec_device_count(void);

@@ -354,3 +354,37 @@ def test_concurrent_encode_single(oracle):
     [t.start() for t in th]
     [t.join() for t in th]
     assert not errors
+
+
+def _pinned(lib, nbytes):
+    p = lib.ec_host_alloc(nbytes)
+    assert p
+    arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+    return p, arr
+
+
+def test_host_pipeline_encode_rebuild(oracle):
+    """ec_encode_segments_host / ec_rebuild_segments_host: pinned host
+    buffers in and out, 3-stream H2D/kernel/D2H ring (end-to-end path)."""
+    lib = _native.load()
+    k, n, ess, stripes, nseg = 20, 60, 4096, 9, 5
+    sch = scheme(k, n, ess)
+    spad, plen = stripes * k * ess, stripes * ess
+    ps, segs = _pinned(lib, nseg * spad)
+    segs[:] = np.random.default_rng(31).integers(0, 256, nseg * spad, dtype=np.uint8)
+    pp, pieces = _pinned(lib, nseg * n * plen)
+    po, out = _pinned(lib, nseg * spad)
+    try:
+        assert lib.ec_encode_segments_host(sch.ctx, ps, nseg, stripes, pp, 0) == 0
+        f = oracle.FEC(k, n)
+        for g in range(nseg):
+            ref = f.encode_segment(segs[g * spad:(g + 1) * spad], ess)
+            assert np.array_equal(pieces[g * n * plen:(g + 1) * n * plen].reshape(n, plen), ref)
+        nums = list(range(40, 60))
+        c_nums = (ctypes.c_int * k)(*nums)
+        c_ptrs = (ctypes.c_void_p * k)(*[pp + i * plen for i in nums])
+        assert lib.ec_rebuild_segments_host(sch.ctx, k, c_nums, c_ptrs, stripes, nseg, n * plen, po) == 0
+        assert np.array_equal(out, segs)
+    finally:
+        for p in (ps, pp, po):
+            lib.ec_host_free(p)

@@ -355,6 +355,67 @@ __global__ __launch_bounds__(256, 2) void dec_lc(const RsArgs a) {
     }
 }
 
+
+// warp-specialised rebuild: NC compute waves (OPW rows each) + NL loader
+// waves; LDS ring of 2 slots of JC input shares; one LDS-only barrier per
+// (tile, chunk) item; roles run separate loops with equal barrier counts.
+template <int OPW, int NC, int NL, int JC>
+__global__ __launch_bounds__((NC + NL) * 64, 1) void dec_ws(const RsArgs a) {
+    constexpr int PER = JC / NL;
+    __shared__ uint32_t lds[2][JC * 8 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunk = (a.nin + JC - 1) / JC;
+    const int64_t my_tiles = a.total_tiles > blockIdx.x ? (a.total_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    const int64_t nitems = my_tiles * nchunk;
+    if (wave >= NC) {
+        const int lw = wave - NC;
+        auto stage = [&](int64_t it, int slot) {
+            const int64_t tl = it / nchunk;
+            const int ch = (int)(it - tl * nchunk);
+            const int64_t tile = blockIdx.x + tl * gridDim.x;
+            const int64_t seg = tile / a.tiles_per_seg;
+            const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+            const int j0 = ch * JC;
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            stage_inputs<NL, PER, true>(a, seg, c, lds[slot], lane, lw, j0, jn, true);
+        };
+        if (nitems > 0) stage(0, 0);
+        lds_barrier();
+        for (int64_t it = 0; it < nitems; it++) {
+            if (it + 1 < nitems) stage(it + 1, (int)((it + 1) & 1));
+            lds_barrier();
+        }
+    } else {
+        const int per_wave = (a.nout + NC - 1) / NC;
+        const int rbase = wave * per_wave;
+        int cnt = a.nout - rbase;
+        cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
+        uint32_t acc[OPW][8];
+        lds_barrier();
+        for (int64_t it = 0; it < nitems; it++) {
+            const int64_t tl = it / nchunk;
+            const int ch = (int)(it - tl * nchunk);
+            if (ch == 0) {
+#pragma unroll
+                for (int o = 0; o < OPW; o++)
+#pragma unroll
+                    for (int p = 0; p < 8; p++) acc[o][p] = 0;
+            }
+            const int j0 = ch * JC;
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            if (cnt > 0) compute_generic<OPW>(a, lds[it & 1], lane, j0, jn, rbase, cnt, acc);
+            if (ch == nchunk - 1 && cnt > 0) {
+                const int64_t tile = blockIdx.x + tl * gridDim.x;
+                const int64_t seg = tile / a.tiles_per_seg;
+                const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+                store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+            }
+            lds_barrier();
+        }
+    }
+}
+
 static uint8_t gmul(uint8_t a, uint8_t b) { return gf_mul(a, b); }
 
 int main(int argc, char **argv) {
@@ -430,10 +491,13 @@ int main(int argc, char **argv) {
         };
         {
             const int grid = cus * 4;
-            timeit("OLD bitbranch JC16 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 2, 16>), dim3(grid), dim3(256), 0, 0, a); });
-            timeit("LDS-coef bitbranch grid4x", [&] { hipLaunchKernelGGL((dec_lc<8, 5, 16>), dim3(grid), dim3(256), 0, 0, a); });
-            timeit("LDS-coef nibble-switch grid4x", [&] { hipLaunchKernelGGL((dec_lc<8, 6, 16>), dim3(grid), dim3(256), 0, 0, a); });
-            timeit("LDS-coef nibble-switch grid2x", [&] { hipLaunchKernelGGL((dec_lc<8, 6, 16>), dim3(cus * 2), dim3(256), 0, 0, a); });
+            timeit("product-like NW8 OPW4 grid4x", [&] { hipLaunchKernelGGL((dec_plain<4, 0, 16, 8>), dim3(grid), dim3(512), 0, 0, a); });
+            timeit("ws 8c+4l JC16 grid2x", [&] { hipLaunchKernelGGL((dec_ws<4, 8, 4, 16>), dim3(cus * 2), dim3(768), 0, 0, a); });
+            timeit("ws 8c+4l JC16 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 8, 4, 16>), dim3(cus), dim3(768), 0, 0, a); });
+            timeit("ws 12c+4l JC16 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 12, 4, 16>), dim3(cus), dim3(1024), 0, 0, a); });
+            timeit("ws 12c+4l JC32 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 12, 4, 32>), dim3(cus), dim3(1024), 0, 0, a); });
+            timeit("ws 8c+4l JC32 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 8, 4, 32>), dim3(cus), dim3(768), 0, 0, a); });
+            timeit("ws 4c+4l OPW8 JC32 grid1x", [&] { hipLaunchKernelGGL((dec_ws<8, 4, 4, 32>), dim3(cus), dim3(512), 0, 0, a); });
         }
         CK(hipFree(dcoef));
     }

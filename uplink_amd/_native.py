@@ -55,6 +55,11 @@ SIGNATURES = {
     "ec_rebuild_segments_batched": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_size_t,
                                                    ctypes.c_longlong, ctypes.c_longlong, vp, vp]),
+    "ec_encode_segments_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, ctypes.c_int]),
+    "ec_rebuild_segments_host": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                                ctypes.c_size_t, ctypes.c_size_t, ctypes.c_longlong, vp]),
+    "ec_host_alloc": (vp, [ctypes.c_size_t]),
+    "ec_host_free": (None, [vp]),
     "ec_device_count": (ctypes.c_int, []),
     "ec_set_device": (ctypes.c_int, [ctypes.c_int]),
     "ec_encode_kernel_name": (ctypes.c_char_p, [vp]),

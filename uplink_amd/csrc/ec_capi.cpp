@@ -45,8 +45,18 @@ struct Workspace {
 
 }  // namespace
 
+struct HostPipe {
+    static constexpr int kSlots = 3;
+    hipStream_t st[kSlots] = {};
+    uint8_t *d_in[kSlots] = {};
+    uint8_t *d_out[kSlots] = {};
+    size_t in_cap = 0, out_cap = 0;
+};
+
 struct ec_ctx {
     int k = 0, n = 0, ess = 0, device = 0;
+    std::mutex pipe_mu;  // one host pipeline at a time per context
+    HostPipe pipe;
     std::vector<uint8_t> G;        // n x k
     uint8_t *d_coef_all = nullptr; // [j][i] = G[i][j], ld = ld_all
     int ld_all = 0;
@@ -283,6 +293,11 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
 
 void ec_destroy(ec_ctx *c) {
     if (!c) return;
+    for (int s = 0; s < HostPipe::kSlots; s++) {
+        if (c->pipe.st[s]) (void)hipStreamSynchronize(c->pipe.st[s]), (void)hipStreamDestroy(c->pipe.st[s]);
+        if (c->pipe.d_in[s]) (void)hipFree(c->pipe.d_in[s]);
+        if (c->pipe.d_out[s]) (void)hipFree(c->pipe.d_out[s]);
+    }
     c->plans.clear();
     for (auto &w : c->all_ws) {
         if (w->stream) (void)hipStreamSynchronize(w->stream), (void)hipStreamDestroy(w->stream);
@@ -412,6 +427,36 @@ int ec_rebuild_segments(const ec_ctx *c, int nshares, const int *nums, const uin
     return ec_rebuild_segments_batched(c, nshares, nums, pieces, nstripes, 1, 0, 0, out, stream);
 }
 
+// ---------------------------------------------------------------- host pipeline
+static int pipe_reserve(ec_ctx *c, size_t in_bytes, size_t out_bytes) {
+    HostPipe &p = c->pipe;
+    for (int s = 0; s < HostPipe::kSlots; s++)
+        if (!p.st[s]) HIP_TRY(hipStreamCreateWithFlags(&p.st[s], hipStreamNonBlocking));
+    if (p.in_cap < in_bytes) {
+        for (int s = 0; s < HostPipe::kSlots; s++) {
+            if (p.d_in[s]) (void)hipFree(p.d_in[s]);
+            p.d_in[s] = nullptr;
+            HIP_TRY(hipMalloc(&p.d_in[s], in_bytes));
+        }
+        p.in_cap = in_bytes;
+    }
+    if (p.out_cap < out_bytes) {
+        for (int s = 0; s < HostPipe::kSlots; s++) {
+            if (p.d_out[s]) (void)hipFree(p.d_out[s]);
+            p.d_out[s] = nullptr;
+            HIP_TRY(hipMalloc(&p.d_out[s], out_bytes));
+        }
+        p.out_cap = out_bytes;
+    }
+    return EC_OK;
+}
+
+static int pipe_drain(ec_ctx *c, int rc) {
+    for (int s = 0; s < HostPipe::kSlots; s++)
+        if (c->pipe.st[s] && hipStreamSynchronize(c->pipe.st[s]) != hipSuccess && rc == EC_OK) rc = EC_ERR_DEVICE;
+    return rc;
+}
+
 // ---------------------------------------------------------------- per-stripe
 int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len, int num) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
@@ -538,6 +583,84 @@ int ec_rebuild(const ec_ctx *cc, int nshares, int *nums, const uint8_t **shares,
 // shares beyond the first k (sorted) are re-encoded from the first k on the
 // GPU, mismatching byte columns are flagged, and each flagged column is
 // corrected by Berlekamp-Welch on the GPU; shares are corrected in place.
+void *ec_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void ec_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+// Segment g goes through slot g % 3: H2D on that slot's stream, then the
+// kernel, then D2H, all stream-ordered, so a slot's device buffers are never
+// reused before its previous segment has left the GPU; the three streams
+// overlap the copies of neighbouring segments with each other and the kernel.
+int ec_encode_segments_host(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                            int flags) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    const size_t spad = nstripes * (size_t)c->k * c->ess;
+    const int rows = (flags & EC_FLAG_PARITY_ONLY) ? c->n - c->k : c->n;
+    const size_t pbytes = (size_t)rows * nstripes * c->ess;
+    std::lock_guard<std::mutex> g(c->pipe_mu);
+    int rc = pipe_reserve(c, spad, pbytes);
+    if (rc) return rc;
+    for (size_t s = 0; s < nseg && rc == EC_OK; s++) {
+        const int slot = (int)(s % HostPipe::kSlots);
+        hipStream_t st = c->pipe.st[slot];
+        if (hipMemcpyAsync(c->pipe.d_in[slot], segs + s * spad, spad, hipMemcpyHostToDevice, st) != hipSuccess) {
+            rc = EC_ERR_DEVICE;
+            break;
+        }
+        rc = ec_encode_segments(c, c->pipe.d_in[slot], 1, nstripes, c->pipe.d_out[slot], flags, st);
+        if (rc) break;
+        if (hipMemcpyAsync(pieces + s * pbytes, c->pipe.d_out[slot], pbytes, hipMemcpyDeviceToHost, st) != hipSuccess)
+            rc = EC_ERR_DEVICE;
+    }
+    return pipe_drain(c, rc);
+}
+
+int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, const uint8_t *const *pieces,
+                             size_t nstripes, size_t nseg, long long piece_seg_stride, uint8_t *out) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !nums || !pieces || !out) return EC_ERR_INVALID_ARG;
+    if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    const size_t plen = nstripes * c->ess;
+    const size_t spad = nstripes * (size_t)c->k * c->ess;
+    std::lock_guard<std::mutex> g(c->pipe_mu);
+    rc = pipe_reserve(c, plen * c->k, spad);
+    if (rc) return rc;
+    std::vector<int> knums(c->k);
+    for (size_t s = 0; s < nseg && rc == EC_OK; s++) {
+        const int slot = (int)(s % HostPipe::kSlots);
+        hipStream_t st = c->pipe.st[slot];
+        std::vector<const uint8_t *> dptr(c->k);
+        for (int i = 0; i < c->k; i++) {
+            const uint8_t *src = pieces[order[i]] + (int64_t)s * piece_seg_stride;
+            if (hipMemcpyAsync(c->pipe.d_in[slot] + plen * i, src, plen, hipMemcpyHostToDevice, st) != hipSuccess) {
+                rc = EC_ERR_DEVICE;
+                break;
+            }
+            dptr[i] = c->pipe.d_in[slot] + plen * i;
+            knums[i] = ids[i];
+        }
+        if (rc) break;
+        rc = rebuild_device(c, c->k, knums.data(), dptr.data(), c->ess, (int64_t)nstripes, 1, 0, 0,
+                            c->pipe.d_out[slot], st);
+        if (rc) break;
+        if (hipMemcpyAsync(out + s * spad, c->pipe.d_out[slot], spad, hipMemcpyDeviceToHost, st) != hipSuccess)
+            rc = EC_ERR_DEVICE;
+    }
+    return pipe_drain(c, rc);
+}
+
 int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
