@@ -15,6 +15,41 @@ using namespace uplink_ec::dev;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
+// acc ^= (bit B of c ? y : 0) ^ (bit B+1 of c ? z : 0) with wave-uniform scalar
+// branches and one v_bitop3 per plane when both bits are set.
+template <int B>
+__device__ __forceinline__ void pair_add_asm(uint32_t (&acc)[8], const uint32_t (&y)[8], const uint32_t (&z)[8],
+                                             uint32_t c) {
+#define PA_OPS(op, src) \
+    op " %[a0], %[a0], %[" src "0]\n" op " %[a1], %[a1], %[" src "1]\n" op " %[a2], %[a2], %[" src "2]\n" \
+    op " %[a3], %[a3], %[" src "3]\n" op " %[a4], %[a4], %[" src "4]\n" op " %[a5], %[a5], %[" src "5]\n" \
+    op " %[a6], %[a6], %[" src "6]\n" op " %[a7], %[a7], %[" src "7]\n"
+#define PA_BOTH(i) "v_bitop3_b32 %[a" #i "], %[a" #i "], %[y" #i "], %[z" #i "] bitop3:0x96\n"
+    asm volatile(
+        "s_bitcmp1_b32 %[c], %[b0]\n"
+        "s_cbranch_scc0 .Lno0_%=\n"
+        "s_bitcmp1_b32 %[c], %[b1]\n"
+        "s_cbranch_scc0 .Lonly0_%=\n"
+        PA_BOTH(0) PA_BOTH(1) PA_BOTH(2) PA_BOTH(3) PA_BOTH(4) PA_BOTH(5) PA_BOTH(6) PA_BOTH(7)
+        "s_branch .Lend_%=\n"
+        ".Lonly0_%=:\n"
+        PA_OPS("v_xor_b32", "y")
+        "s_branch .Lend_%=\n"
+        ".Lno0_%=:\n"
+        "s_bitcmp1_b32 %[c], %[b1]\n"
+        "s_cbranch_scc0 .Lend_%=\n"
+        PA_OPS("v_xor_b32", "z")
+        ".Lend_%=:\n"
+        : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [a4] "+v"(acc[4]),
+          [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7])
+        : [y0] "v"(y[0]), [y1] "v"(y[1]), [y2] "v"(y[2]), [y3] "v"(y[3]), [y4] "v"(y[4]), [y5] "v"(y[5]),
+          [y6] "v"(y[6]), [y7] "v"(y[7]), [z0] "v"(z[0]), [z1] "v"(z[1]), [z2] "v"(z[2]), [z3] "v"(z[3]),
+          [z4] "v"(z[4]), [z5] "v"(z[5]), [z6] "v"(z[6]), [z7] "v"(z[7]), [c] "s"(c), [b0] "i"(B), [b1] "i"(B + 1)
+        : "scc");
+#undef PA_OPS
+#undef PA_BOTH
+}
+
 // MODE 0: branchy bit pairs (product); 1: dense SGPR masks over the y chain;
 // 2: one branch per coefficient bit
 template <int OPW, int MODE>
@@ -22,6 +57,62 @@ __device__ __forceinline__ void body(const RsArgs &a, const uint32_t *lds, int l
                                      int cnt, uint32_t (&acc)[OPW][8]) {
     if constexpr (MODE == 0) {
         compute_generic<OPW>(a, lds, lane, jbase, jn, rbase, cnt, acc);
+        return;
+    }
+    if constexpr (MODE == 8) {
+        for (int jj = 0; jj < jn; jj++) {
+            uint32_t y[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) y[p] = lds[(jj * 8 + p) * 64 + lane];
+            const uint8_t *cp = a.coef + (int64_t)(jbase + jj) * a.coef_ld + rbase;
+            uint32_t cw[(OPW + 3) / 4];
+#pragma unroll
+            for (int q = 0; q < (OPW + 3) / 4; q++) cw[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * q));
+            static_for<4>([&]<int G>() {
+                uint32_t y2[8];
+                mul2_planes(y, y2);
+                static_for<OPW>([&]<int O>() {
+                    if (O < cnt) pair_add_asm<8 * (O % 4) + 2 * G>(acc[O], y, y2, cw[O / 4]);
+                });
+                if constexpr (G < 3) mul2_planes(y2, y);
+            });
+        }
+        return;
+    }
+    if constexpr (MODE == 7) {
+        // nested single-bit scalar branches over bit pairs; both set -> one v_bitop3
+        for (int jj = 0; jj < jn; jj++) {
+            uint32_t y[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) y[p] = lds[(jj * 8 + p) * 64 + lane];
+            const uint8_t *cp = a.coef + (int64_t)(jbase + jj) * a.coef_ld + rbase;
+            uint32_t cw[(OPW + 3) / 4];
+#pragma unroll
+            for (int q = 0; q < (OPW + 3) / 4; q++) cw[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * q));
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                uint32_t y2[8];
+                mul2_planes(y, y2);
+                static_for<OPW>([&]<int O>() {
+                    if (O < cnt) {
+                        const uint32_t two = (cw[O / 4] >> (8 * (O % 4) + 2 * g)) & 3u;
+                        if (two == 3u) {
+#pragma unroll
+                            for (int p = 0; p < 8; p++) acc[O][p] = __builtin_amdgcn_bitop3_b32(acc[O][p], y[p], y2[p], 0x96);
+                        }
+                        if (two == 1u) {
+#pragma unroll
+                            for (int p = 0; p < 8; p++) acc[O][p] ^= y[p];
+                        }
+                        if (two == 2u) {
+#pragma unroll
+                            for (int p = 0; p < 8; p++) acc[O][p] ^= y2[p];
+                        }
+                    }
+                });
+                if (g < 3) mul2_planes(y2, y);
+            }
+        }
         return;
     }
     if constexpr (MODE == 4) {
@@ -491,13 +582,11 @@ int main(int argc, char **argv) {
         };
         {
             const int grid = cus * 4;
-            timeit("product-like NW8 OPW4 grid4x", [&] { hipLaunchKernelGGL((dec_plain<4, 0, 16, 8>), dim3(grid), dim3(512), 0, 0, a); });
-            timeit("ws 8c+4l JC16 grid2x", [&] { hipLaunchKernelGGL((dec_ws<4, 8, 4, 16>), dim3(cus * 2), dim3(768), 0, 0, a); });
-            timeit("ws 8c+4l JC16 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 8, 4, 16>), dim3(cus), dim3(768), 0, 0, a); });
-            timeit("ws 12c+4l JC16 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 12, 4, 16>), dim3(cus), dim3(1024), 0, 0, a); });
-            timeit("ws 12c+4l JC32 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 12, 4, 32>), dim3(cus), dim3(1024), 0, 0, a); });
-            timeit("ws 8c+4l JC32 grid1x", [&] { hipLaunchKernelGGL((dec_ws<4, 8, 4, 32>), dim3(cus), dim3(768), 0, 0, a); });
-            timeit("ws 4c+4l OPW8 JC32 grid1x", [&] { hipLaunchKernelGGL((dec_ws<8, 4, 4, 32>), dim3(cus), dim3(512), 0, 0, a); });
+            for (int rep = 0; rep < 2; rep++) {
+            timeit("product NW8 OPW4 grid4x", [&] { hipLaunchKernelGGL((dec_plain<4, 0, 16, 8>), dim3(grid), dim3(512), 0, 0, a); });
+            timeit("asm-pairs NW8 OPW4 grid4x", [&] { hipLaunchKernelGGL((dec_plain<4, 8, 16, 8>), dim3(grid), dim3(512), 0, 0, a); });
+            timeit("asm-pairs NW4 OPW8 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 8, 16, 4>), dim3(grid), dim3(256), 0, 0, a); });
+            }
         }
         CK(hipFree(dcoef));
     }

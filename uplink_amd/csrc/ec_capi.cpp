@@ -69,6 +69,8 @@ struct ec_ctx {
 namespace {
 
 constexpr size_t kMaxPlans = 64;
+// coefficient rows are read as whole 32-bit words past the last row (OPW slots)
+constexpr size_t kCoefPad = 64;
 
 int round16(int x) { return (x + 15) & ~15; }
 
@@ -200,7 +202,7 @@ int get_plan(ec_ctx *c, const std::vector<int> &ids, PlanPtr *out) {
         if (ids[i] >= k) p->missing.push_back(i);
     const int R = (int)p->missing.size();
     p->coef_ld = round16(std::max(R, 1));
-    std::vector<uint8_t> coef((size_t)k * p->coef_ld, 0);
+    std::vector<uint8_t> coef((size_t)k * p->coef_ld + kCoefPad, 0);
     for (int r = 0; r < R; r++)
         for (int col = 0; col < k; col++) coef[(size_t)col * p->coef_ld + r] = m[(size_t)p->missing[r] * k + col];
     HIP_TRY(hipMalloc(&p->d_coef, coef.size()));
@@ -282,7 +284,7 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     for (int i = 0; i < n; i++)
         for (int j = 0; j < k; j++) c->G[(size_t)i * k + j] = gen_entry(k, i, j);
     c->ld_all = round16(n);
-    std::vector<uint8_t> coef((size_t)k * c->ld_all, 0);
+    std::vector<uint8_t> coef((size_t)k * c->ld_all + kCoefPad, 0);
     for (int j = 0; j < k; j++)
         for (int i = 0; i < n; i++) coef[(size_t)j * c->ld_all + i] = c->G[(size_t)i * k + j];
     HIP_TRY(hipMalloc(&c->d_coef_all, coef.size()));
@@ -694,7 +696,7 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
             for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[i] * k], k);
             if (!gf_invert(m.data(), k)) { rc = EC_ERR_SINGULAR; break; }
             const int ld = round16(extra);
-            std::vector<uint8_t> coef((size_t)k * ld, 0);
+            std::vector<uint8_t> coef((size_t)k * ld + kCoefPad, 0);
             for (int r = 0; r < extra; r++)
                 for (int col = 0; col < k; col++) {
                     uint8_t acc = 0;

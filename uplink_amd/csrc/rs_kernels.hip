@@ -98,11 +98,13 @@ __global__ __launch_bounds__(kThreads, 1) void rs_encode_special(const RsArgs a)
 
 // Runtime-matrix kernel (rebuild, and encode for (k, n) without a
 // specialised kernel).  Compute-bound (the decode matrix is data), so every
-// wave computes (no loader waves) and four workgroups share a CU; inputs
-// are staged in LDS chunks of kGenericJC shares; each of the NW waves owns
-// ceil(nout / NW) rows (<= OPW) of a pass.  8 waves x 4 rows (77 VGPRs, 6
-// waves/SIMD) beat 4 waves x 8 rows for decode (69 vs 80 us per RS(29,80)
-// 64 MiB segment at m = 29, tools/exp/decode_exp.hip).
+// wave computes (no loader waves) and several workgroups share a CU; inputs
+// are staged in LDS chunks of kGenericJC shares.  The rows of a pass are
+// spread evenly over the NW waves (counts differ by at most one, <= OPW) and
+// the row group of a wave is rotated by blockIdx so the SIMDs of a CU, which
+// host waves of several workgroups, get equal VALU work.  4 waves x 8 rows
+// beat 8 x 4 (72 vs 73 us at m = 29, 57 vs 64 us at m = 17 per RS(29,80)
+// 64 MiB segment: tools/exp/decode_exp.hip).
 constexpr int kGenericJC = 16;
 
 template <int OPW, int NW>
@@ -112,17 +114,15 @@ __global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) 
     __shared__ uint32_t lds[JC * 8 * 64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int per_wave = (a.nout + NW - 1) / NW;
-    per_wave = per_wave > OPW ? OPW : per_wave;
-    const int rows_per_pass = NW * per_wave;
-    const int npass = (a.nout > 0 && rows_per_pass > 0) ? (a.nout + rows_per_pass - 1) / rows_per_pass : 1;
+    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
+    const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
         const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
         for (int pass = 0; pass < npass; pass++) {
-            const int rbase = pass * rows_per_pass + wave * per_wave;
-            int cnt = a.nout - rbase;
-            cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
+            const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
+            const int rbase = p0 + group * prow / NW;
+            const int cnt = p0 + (group + 1) * prow / NW - rbase;
             uint32_t acc[OPW][8];
 #pragma unroll
             for (int o = 0; o < OPW; o++)
@@ -223,8 +223,8 @@ hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStr
 
 hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
     if (grid <= 0) grid = default_grid(a.total_tiles, 4);
-    if (a.nout <= 8 * 4)
-        hipLaunchKernelGGL((rs_matmul_generic<4, 8>), dim3(grid), dim3(8 * 64), 0, s, a);
+    if (a.nout <= 4 * 8)
+        hipLaunchKernelGGL((rs_matmul_generic<8, 4>), dim3(grid), dim3(4 * 64), 0, s, a);
     else if (a.nout <= 4 * 16)
         hipLaunchKernelGGL((rs_matmul_generic<16, 4>), dim3(grid), dim3(4 * 64), 0, s, a);
     else
