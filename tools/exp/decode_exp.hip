@@ -50,13 +50,36 @@ __device__ __forceinline__ void pair_add_asm(uint32_t (&acc)[8], const uint32_t 
 #undef PA_BOTH
 }
 
+
+
 // MODE 0: branchy bit pairs (product); 1: dense SGPR masks over the y chain;
 // 2: one branch per coefficient bit
 template <int OPW, int MODE>
 __device__ __forceinline__ void body(const RsArgs &a, const uint32_t *lds, int lane, int jbase, int jn, int rbase,
                                      int cnt, uint32_t (&acc)[OPW][8]) {
-    if constexpr (MODE == 0) {
-        compute_generic<OPW>(a, lds, lane, jbase, jn, rbase, cnt, acc);
+    if constexpr (MODE == 9 || MODE == 0) {  // 0: same body as 9 (product moved to LDS coefficients)
+        for (int jj = 0; jj < jn; jj++) {
+            uint32_t y0[8], y1[8], y2[8], y3[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) y0[p] = lds[(jj * 8 + p) * 64 + lane];
+            const uint8_t *cp = a.coef + (int64_t)(jbase + jj) * a.coef_ld + rbase;
+            uint32_t cw[(OPW + 3) / 4];
+#pragma unroll
+            for (int q = 0; q < (OPW + 3) / 4; q++) cw[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * q));
+            mul2_planes(y0, y1);
+            mul2_planes(y1, y2);
+            mul2_planes(y2, y3);
+            static_for<OPW>([&]<int O>() {
+                if (O < cnt) add_nibble<8 * (O % 4)>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+            });
+            mul2_planes(y3, y0);
+            mul2_planes(y0, y1);
+            mul2_planes(y1, y2);
+            mul2_planes(y2, y3);
+            static_for<OPW>([&]<int O>() {
+                if (O < cnt) add_nibble<8 * (O % 4) + 4>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+            });
+        }
         return;
     }
     if constexpr (MODE == 8) {
@@ -206,13 +229,12 @@ __global__ __launch_bounds__(NW * 64, 2) void dec_plain(const RsArgs a) {
     __shared__ uint32_t lds[JC * 8 * 64];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int per_wave = (a.nout + NW - 1) / NW;
+    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
         const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
-        const int rbase = wave * per_wave;
-        int cnt = a.nout - rbase;
-        cnt = cnt < 0 ? 0 : (cnt > per_wave ? per_wave : cnt);
+        const int rbase = group * a.nout / NW;
+        const int cnt = (group + 1) * a.nout / NW - rbase;
         uint32_t acc[OPW][8];
 #pragma unroll
         for (int o = 0; o < OPW; o++)
@@ -229,6 +251,170 @@ __global__ __launch_bounds__(NW * 64, 2) void dec_plain(const RsArgs a) {
     }
 }
 
+
+// Register prefetch: the raw 16-B chunks of the next work item (tile, chunk)
+// are loaded into VGPRs before computing the current one, so global-load
+// latency hides behind the XOR work; LDS holds one bit-sliced chunk.
+template <int PER>
+struct RawChunk {
+    uint4 A[PER], B[PER];
+};
+
+template <int NW, int PER>
+__device__ __forceinline__ void pf_load(const RsArgs &a, int64_t seg, const TileCols &c, int wave, int j0, int jn,
+                                        RawChunk<PER> &r) {
+    const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int j = wave + NW * i;
+        if (j < jn) {
+            const uint8_t *p = in_seg + a.in_off[j0 + j];
+            r.A[i] = c.vA ? ld16<true>(p + c.inA) : z;
+            r.B[i] = c.vB ? ld16<true>(p + c.inB) : z;
+        }
+    }
+}
+
+template <int NW, int PER>
+__device__ __forceinline__ void pf_commit(const RsArgs &a, int64_t seg, const TileCols &c, uint32_t *lds, int lane,
+                                          int wave, int j0, int jn, const RawChunk<PER> &r) {
+    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int j = wave + NW * i;
+        if (j < jn) {
+            const int64_t co = a.copy_off[j0 + j];
+            if (co >= 0) {
+                uint8_t *p = out_seg + co;
+                if (c.vA) st16<true>(p + c.outA, r.A[i].x, r.A[i].y, r.A[i].z, r.A[i].w);
+                if (c.vB) st16<true>(p + c.outB, r.B[i].x, r.B[i].y, r.B[i].z, r.B[i].w);
+            }
+            uint32_t w[8] = {r.A[i].x, r.A[i].y, r.A[i].z, r.A[i].w, r.B[i].x, r.B[i].y, r.B[i].z, r.B[i].w};
+            bitslice8(w);
+            uint32_t *dst = lds + j * 8 * 64 + lane;
+#pragma unroll
+            for (int p = 0; p < 8; p++) dst[p * 64] = w[p];
+        }
+    }
+}
+
+template <int OPW, int MODE, int JC, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void dec_pf(const RsArgs a) {
+    constexpr int PER = JC / NW;
+    __shared__ uint32_t lds[JC * 8 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
+    const int rbase = group * a.nout / NW;
+    const int cnt = (group + 1) * a.nout / NW - rbase;
+    const int nchunk = (a.nin + JC - 1) / JC;
+    int64_t tile = blockIdx.x;
+    if (tile >= a.total_tiles) return;
+    int64_t seg = tile / a.tiles_per_seg;
+    TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+    RawChunk<PER> raw;
+    pf_load<NW, PER>(a, seg, c, wave, 0, a.nin < JC ? a.nin : JC, raw);
+    uint32_t acc[OPW][8];
+    int ch = 0;
+    while (true) {
+        const int j0 = ch * JC;
+        const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+        if (ch == 0) {
+#pragma unroll
+            for (int o = 0; o < OPW; o++)
+#pragma unroll
+                for (int p = 0; p < 8; p++) acc[o][p] = 0;
+        }
+        pf_commit<NW, PER>(a, seg, c, lds, lane, wave, j0, jn, raw);
+        lds_barrier();
+        // prefetch the next item
+        int nch = ch + 1;
+        int64_t ntile = tile;
+        if (nch == nchunk) { nch = 0; ntile = tile + gridDim.x; }
+        int64_t nseg = seg;
+        TileCols nc = c;
+        if (ntile < a.total_tiles) {
+            if (ntile != tile) {
+                nseg = ntile / a.tiles_per_seg;
+                nc = tile_cols(a, ntile - nseg * a.tiles_per_seg, lane);
+            }
+            const int nj0 = nch * JC;
+            pf_load<NW, PER>(a, nseg, nc, wave, nj0, a.nin - nj0 < JC ? a.nin - nj0 : JC, raw);
+        }
+        if (cnt > 0) body<OPW, MODE>(a, lds, lane, j0, jn, rbase, cnt, acc);
+        if (ch == nchunk - 1) store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+        lds_barrier();
+        if (ntile >= a.total_tiles) break;
+        ch = nch;
+        tile = ntile;
+        seg = nseg;
+        c = nc;
+    }
+}
+
+// Coefficients staged once per workgroup in LDS as [j][group][8 bytes]
+// (zero-padded), read per input with one broadcast ds_read_b64: no global
+// load (and no vmcnt wait behind outstanding stores) inside the j loop.
+template <int OPW>
+__device__ __forceinline__ void body_lc(const uint32_t *lds, const uint2 *lcoef, int lane, int jn, int jbase, int group,
+                                        int NWr, int cnt, uint32_t (&acc)[OPW][8]) {
+    static_assert(OPW == 8, "one 8-byte coefficient slot per wave");
+    for (int jj = 0; jj < jn; jj++) {
+        uint32_t y0[8], y1[8], y2[8], y3[8];
+#pragma unroll
+        for (int p = 0; p < 8; p++) y0[p] = lds[(jj * 8 + p) * 64 + lane];
+        const uint2 cv = lcoef[(jbase + jj) * NWr + group];
+        uint32_t cw[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(cv.x), (uint32_t)__builtin_amdgcn_readfirstlane(cv.y)};
+        mul2_planes(y0, y1);
+        mul2_planes(y1, y2);
+        mul2_planes(y2, y3);
+        static_for<OPW>([&]<int O>() {
+            if (O < cnt) add_nibble<8 * (O % 4)>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+        });
+        mul2_planes(y3, y0);
+        mul2_planes(y0, y1);
+        mul2_planes(y1, y2);
+        mul2_planes(y2, y3);
+        static_for<OPW>([&]<int O>() {
+            if (O < cnt) add_nibble<8 * (O % 4) + 4>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+        });
+    }
+}
+
+template <int OPW, int JC, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void dec_lc2(const RsArgs a) {
+    constexpr int PER = JC / NW;
+    __shared__ uint32_t lds[JC * 8 * 64];
+    __shared__ uint2 lcoef[64 * NW];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
+    const int rbase = group * a.nout / NW;
+    const int cnt = (group + 1) * a.nout / NW - rbase;
+    for (int t = threadIdx.x; t < a.nin * NW * 8; t += NW * 64) {
+        const int j = t / (NW * 8), g = (t / 8) % NW, o = t % 8;
+        const int rb = g * a.nout / NW, cn = (g + 1) * a.nout / NW - rb;
+        ((uint8_t *)lcoef)[t] = o < cn ? a.coef[(int64_t)j * a.coef_ld + rb + o] : 0;
+    }
+    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const int64_t seg = tile / a.tiles_per_seg;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        uint32_t acc[OPW][8];
+#pragma unroll
+        for (int o = 0; o < OPW; o++)
+#pragma unroll
+            for (int p = 0; p < 8; p++) acc[o][p] = 0;
+        for (int j0 = 0; j0 < a.nin; j0 += JC) {
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, true);
+            __syncthreads();
+            if (cnt > 0) body_lc<OPW>(lds, lcoef, lane, jn, j0, group, NW, cnt, acc);
+            __syncthreads();
+        }
+        store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+    }
+}
 
 // two tiles (2 x 2048 columns) per WG item: each branch on a coefficient bit
 // guards 16 XORs instead of 8; multiples x*2^b formed on the fly.
@@ -495,7 +681,72 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void dec_ws(const RsArgs a) {
             }
             const int j0 = ch * JC;
             const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
-            if (cnt > 0) compute_generic<OPW>(a, lds[it & 1], lane, j0, jn, rbase, cnt, acc);
+            if (cnt > 0) body<OPW, 9>(a, lds[it & 1], lane, j0, jn, rbase, cnt, acc);
+            if (ch == nchunk - 1 && cnt > 0) {
+                const int64_t tile = blockIdx.x + tl * gridDim.x;
+                const int64_t seg = tile / a.tiles_per_seg;
+                const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+                store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+            }
+            lds_barrier();
+        }
+    }
+}
+
+// Warp-specialised rebuild, v2: per workgroup 4 compute waves (OPW rows
+// each, coefficients from LDS, never wait on vmcnt) + 1 loader wave (global
+// loads, systematic copies, bit-slicing into a 2-slot LDS ring); 4 such
+// workgroups per CU (5 waves/SIMD) so VALU issue has enough waves.
+template <int OPW, int JC>
+__global__ __launch_bounds__(320, 5) void dec_ws2(const RsArgs a) {
+    constexpr int NC = 4;
+    __shared__ uint32_t lds[2][JC * 8 * 64];
+    __shared__ uint2 lcoef[64 * NC];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunk = (a.nin + JC - 1) / JC;
+    const int64_t my_tiles = a.total_tiles > blockIdx.x ? (a.total_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    const int64_t nitems = my_tiles * nchunk;
+    for (int t = threadIdx.x; t < a.nin * NC * 8; t += 320) {
+        const int j = t / (NC * 8), g = (t / 8) % NC, o = t % 8;
+        const int rb = g * a.nout / NC, cn = (g + 1) * a.nout / NC - rb;
+        ((uint8_t *)lcoef)[t] = o < cn ? a.coef[(int64_t)j * a.coef_ld + rb + o] : 0;
+    }
+    if (wave == NC) {
+        auto stage = [&](int64_t it, int slot) {
+            const int64_t tl = it / nchunk;
+            const int ch = (int)(it - tl * nchunk);
+            const int64_t tile = blockIdx.x + tl * gridDim.x;
+            const int64_t seg = tile / a.tiles_per_seg;
+            const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+            const int j0 = ch * JC;
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            stage_inputs<1, JC, true>(a, seg, c, lds[slot], lane, 0, j0, jn, true);
+        };
+        if (nitems > 0) stage(0, 0);
+        lds_barrier();
+        for (int64_t it = 0; it < nitems; it++) {
+            if (it + 1 < nitems) stage(it + 1, (int)((it + 1) & 1));
+            lds_barrier();
+        }
+    } else {
+        const int group = (wave + (int)(blockIdx.x % NC)) % NC;
+        const int rbase = group * a.nout / NC;
+        const int cnt = (group + 1) * a.nout / NC - rbase;
+        uint32_t acc[OPW][8];
+        lds_barrier();
+        for (int64_t it = 0; it < nitems; it++) {
+            const int64_t tl = it / nchunk;
+            const int ch = (int)(it - tl * nchunk);
+            if (ch == 0) {
+#pragma unroll
+                for (int o = 0; o < OPW; o++)
+#pragma unroll
+                    for (int p = 0; p < 8; p++) acc[o][p] = 0;
+            }
+            const int j0 = ch * JC;
+            const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            if (cnt > 0) body_lc<OPW>(lds[it & 1], lcoef, lane, jn, j0, group, NC, cnt, acc);
             if (ch == nchunk - 1 && cnt > 0) {
                 const int64_t tile = blockIdx.x + tl * gridDim.x;
                 const int64_t seg = tile / a.tiles_per_seg;
@@ -583,8 +834,11 @@ int main(int argc, char **argv) {
         {
             const int grid = cus * 4;
             for (int rep = 0; rep < 2; rep++) {
-            timeit("product NW8 OPW4 grid4x", [&] { hipLaunchKernelGGL((dec_plain<4, 0, 16, 8>), dim3(grid), dim3(512), 0, 0, a); });
-            timeit("asm-pairs NW8 OPW4 grid4x", [&] { hipLaunchKernelGGL((dec_plain<4, 8, 16, 8>), dim3(grid), dim3(512), 0, 0, a); });
+            timeit("product NW4 OPW8 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 0, 16, 4>), dim3(grid), dim3(256), 0, 0, a); });
+            timeit("lds-coef nibble JC8 NW4 OPW8 grid4x", [&] { hipLaunchKernelGGL((dec_lc2<8, 8, 4>), dim3(grid), dim3(256), 0, 0, a); });
+            timeit("ws2 4C+1L JC8 OPW8 grid4x", [&] { hipLaunchKernelGGL((dec_ws2<8, 8>), dim3(grid), dim3(320), 0, 0, a); });
+            timeit("ws2 4C+1L JC8 OPW8 grid8x", [&] { hipLaunchKernelGGL((dec_ws2<8, 8>), dim3(cus * 8), dim3(320), 0, 0, a); });
+            timeit("ws2 4C+1L JC4 OPW8 grid4x", [&] { hipLaunchKernelGGL((dec_ws2<8, 4>), dim3(grid), dim3(320), 0, 0, a); });
             timeit("asm-pairs NW4 OPW8 grid4x", [&] { hipLaunchKernelGGL((dec_plain<8, 8, 16, 4>), dim3(grid), dim3(256), 0, 0, a); });
             }
         }

@@ -221,74 +221,49 @@ __device__ __forceinline__ void mul2_planes(const uint32_t (&o)[8], uint32_t (&n
     n[7] = o[6];
 }
 
-// acc ^= (bit B of c ? y : 0) ^ (bit B+1 of c ? z : 0), c wave-uniform.
-// Two scalar tests pick one of three 8-instruction blocks: v_bitop3 XOR3 when
-// both bits are set (one VALU per plane for two terms), v_xor otherwise.
-// Written as one asm block so the branch structure stays scalar (the
-// compiler's structurizer turned the C++ form into exec-masked code with
-// ~300 extra v_mov per body: tools/exp/decode_exp.hip, MODE 7 vs 8).
-template <int B>
-__device__ __forceinline__ void add_bit_pair(uint32_t (&acc)[8], const uint32_t (&y)[8], const uint32_t (&z)[8],
-                                             uint32_t c) {
-#define UEC_PAIR_XOR(src)                                                                                      \
-    "v_xor_b32 %[a0], %[a0], %[" src "0]\n v_xor_b32 %[a1], %[a1], %[" src "1]\n"                            \
-    "v_xor_b32 %[a2], %[a2], %[" src "2]\n v_xor_b32 %[a3], %[a3], %[" src "3]\n"                            \
-    "v_xor_b32 %[a4], %[a4], %[" src "4]\n v_xor_b32 %[a5], %[a5], %[" src "5]\n"                            \
-    "v_xor_b32 %[a6], %[a6], %[" src "6]\n v_xor_b32 %[a7], %[a7], %[" src "7]\n"
-#define UEC_PAIR_X3(i) "v_bitop3_b32 %[a" #i "], %[a" #i "], %[y" #i "], %[z" #i "] bitop3:0x96\n"
-    asm volatile(
-        "s_bitcmp1_b32 %[c], %[b0]\n"
-        "s_cbranch_scc0 .Lpair_no0_%=\n"
-        "s_bitcmp1_b32 %[c], %[b1]\n"
-        "s_cbranch_scc0 .Lpair_only0_%=\n"
-        UEC_PAIR_X3(0) UEC_PAIR_X3(1) UEC_PAIR_X3(2) UEC_PAIR_X3(3)
-        UEC_PAIR_X3(4) UEC_PAIR_X3(5) UEC_PAIR_X3(6) UEC_PAIR_X3(7)
-        "s_branch .Lpair_end_%=\n"
-        ".Lpair_only0_%=:\n"
-        UEC_PAIR_XOR("y")
-        "s_branch .Lpair_end_%=\n"
-        ".Lpair_no0_%=:\n"
-        "s_bitcmp1_b32 %[c], %[b1]\n"
-        "s_cbranch_scc0 .Lpair_end_%=\n"
-        UEC_PAIR_XOR("z")
-        ".Lpair_end_%=:\n"
-        : [a0] "+v"(acc[0]), [a1] "+v"(acc[1]), [a2] "+v"(acc[2]), [a3] "+v"(acc[3]), [a4] "+v"(acc[4]),
-          [a5] "+v"(acc[5]), [a6] "+v"(acc[6]), [a7] "+v"(acc[7])
-        : [y0] "v"(y[0]), [y1] "v"(y[1]), [y2] "v"(y[2]), [y3] "v"(y[3]), [y4] "v"(y[4]), [y5] "v"(y[5]),
-          [y6] "v"(y[6]), [y7] "v"(y[7]), [z0] "v"(z[0]), [z1] "v"(z[1]), [z2] "v"(z[2]), [z3] "v"(z[3]),
-          [z4] "v"(z[4]), [z5] "v"(z[5]), [z6] "v"(z[6]), [z7] "v"(z[7]), [c] "s"(c), [b0] "i"(B),
-          [b1] "i"(B + 1)
-        : "scc");
-#undef UEC_PAIR_XOR
-#undef UEC_PAIR_X3
-}
+// add_nibble<B>(acc, y0..y3, c): acc ^= ((c >> B) & 15) * x on bit planes,
+// y0..y3 = x*2^i (i = 0..3 of this nibble).  A 4-level tree of wave-uniform
+// scalar bit tests picks one of 16 leaves; a leaf pairs the set bits so two
+// multiples cost one v_bitop3 XOR3 per plane (expected 20 VALU per
+// coefficient byte, vs 24 for fixed bit pairs and 32 for one branch per
+// bit).  One asm block per nibble keeps the branches scalar (the compiler's
+// structurizer turned the C++ forms into exec-masked code with extra moves).
+#include "rs_nibble_tree.inc"
 
-// Runtime-matrix body: for input share j the multiples x*2^b (b = 0..7) are
-// formed on the fly (3 XORs each on bit planes), and for every output row
-// the coefficient's bits are taken in pairs (b, b+1): wave-uniform scalar
-// branches add x*2^b and/or x*2^(b+1) with 8 VALU (expected 6 per pair
-// instead of 8 for one branch per bit).  Measured fastest of the runtime
-// forms tried (per-bit branches, dense SGPR-masked bitop3, C++ 2-bit
-// branches, two tiles per branch): tools/exp/decode_exp.hip.
+// Runtime-matrix body.  For input share j the multiples x*2^b are formed on
+// the fly (3 XORs each on bit planes), four at a time; every output row then
+// walks the nibble tree of its coefficient byte.  The wave's OPW coefficient
+// bytes of input j sit in LDS (staged once per workgroup, zero-padded) and
+// come in with one broadcast LDS read: no global load, and so no vmcnt wait
+// behind outstanding stores, inside the j loop.  Forms measured in
+// tools/exp/decode_exp.hip (RS(29,80), 64 MiB segments, m = 29 / 17 missing):
+// one branch per bit 83/78 us, fixed bit pairs 71/55, nibble tree 66/52,
+// + LDS coefficients 61.5/47.3.
 template <int OPW>
-__device__ __forceinline__ void compute_generic(const RsArgs &a, const uint32_t *lds, int lane, int jbase, int jn,
-                                                int rbase, int cnt, uint32_t (&acc)[OPW][8]) {
+__device__ __forceinline__ void compute_generic(const uint32_t *lds, const uint8_t *lcoef, int coef_stride, int lane,
+                                                int jn, int cnt, uint32_t (&acc)[OPW][8]) {
+    static_assert(OPW % 4 == 0, "coefficient slots are whole words");
+    constexpr int NWORD = OPW / 4;
     for (int jj = 0; jj < jn; jj++) {
-        uint32_t y[8];
+        uint32_t y0[8], y1[8], y2[8], y3[8];
 #pragma unroll
-        for (int p = 0; p < 8; p++) y[p] = lds[(jj * 8 + p) * 64 + lane];
-        const uint8_t *cp = a.coef + (int64_t)(jbase + jj) * a.coef_ld + rbase;
-        uint32_t cw[(OPW + 3) / 4];
+        for (int p = 0; p < 8; p++) y0[p] = lds[(jj * 8 + p) * 64 + lane];
+        const uint32_t *cp = (const uint32_t *)(lcoef + jj * coef_stride);
+        uint32_t cw[NWORD];
 #pragma unroll
-        for (int q = 0; q < (OPW + 3) / 4; q++)
-            cw[q] = __builtin_amdgcn_readfirstlane(*(const uint32_t *)(cp + 4 * q));
-        static_for<4>([&]<int G>() {
-            uint32_t z[8];
-            mul2_planes(y, z);
-            static_for<OPW>([&]<int O>() {
-                if (O < cnt) add_bit_pair<8 * (O % 4) + 2 * G>(acc[O], y, z, cw[O / 4]);
-            });
-            if constexpr (G < 3) mul2_planes(z, y);
+        for (int q = 0; q < NWORD; q++) cw[q] = (uint32_t)__builtin_amdgcn_readfirstlane(cp[q]);
+        mul2_planes(y0, y1);
+        mul2_planes(y1, y2);
+        mul2_planes(y2, y3);
+        static_for<OPW>([&]<int O>() {
+            if (O < cnt) add_nibble<8 * (O % 4)>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+        });
+        mul2_planes(y3, y0);
+        mul2_planes(y0, y1);
+        mul2_planes(y1, y2);
+        mul2_planes(y2, y3);
+        static_for<OPW>([&]<int O>() {
+            if (O < cnt) add_nibble<8 * (O % 4) + 4>(acc[O], y0, y1, y2, y3, cw[O / 4]);
         });
     }
 }

@@ -102,20 +102,34 @@ __global__ __launch_bounds__(kThreads, 1) void rs_encode_special(const RsArgs a)
 // are staged in LDS chunks of kGenericJC shares.  The rows of a pass are
 // spread evenly over the NW waves (counts differ by at most one, <= OPW) and
 // the row group of a wave is rotated by blockIdx so the SIMDs of a CU, which
-// host waves of several workgroups, get equal VALU work.  4 waves x 8 rows
-// beat 8 x 4 (72 vs 73 us at m = 29, 57 vs 64 us at m = 17 per RS(29,80)
-// 64 MiB segment: tools/exp/decode_exp.hip).
-constexpr int kGenericJC = 16;
+// host waves of several workgroups, get equal VALU work.  The coefficients
+// are copied once per workgroup into dynamic LDS as [pass][j][group][OPW]
+// bytes (zero-padded): generic_coef_lds_bytes() gives the size.
+// 4 waves x 8 rows with 8-share chunks measured fastest (61.5 us at m = 29,
+// 47.3 us at m = 17 per RS(29,80) 64 MiB segment: tools/exp/decode_exp.hip).
+constexpr int kGenericJC = 8;
 
 template <int OPW, int NW>
 __global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) {
     constexpr int JC = kGenericJC;
-    constexpr int PER = JC / NW;
+    constexpr int PER = (JC + NW - 1) / NW;
     __shared__ uint32_t lds[JC * 8 * 64];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lcoef[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
+    {
+        const int per_pass = a.nin * NW * OPW;
+        for (int t = threadIdx.x; t < npass * per_pass; t += NW * 64) {
+            const int pass = t / per_pass, r = t - pass * per_pass;
+            const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
+            const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
+            const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
+            lcoef[t] = o < cn ? a.coef[(int64_t)j * a.coef_ld + rb + o] : 0;
+        }
+    }
+    __syncthreads();
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
         const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
@@ -132,12 +146,20 @@ __global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) 
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
                 stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
                 __syncthreads();
-                if (cnt > 0) compute_generic<OPW>(a, lds, lane, j0, jn, rbase, cnt, acc);
+                if (cnt > 0)
+                    compute_generic<OPW>(lds, lcoef + ((pass * a.nin + j0) * NW + group) * OPW, NW * OPW, lane, jn,
+                                         cnt, acc);
                 __syncthreads();
             }
             store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
         }
     }
+}
+
+template <int OPW, int NW>
+size_t generic_coef_lds_bytes(const RsArgs &a) {
+    const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
+    return (size_t)npass * a.nin * NW * OPW;
 }
 
 // ------------------------------------------------ byte-wise fallback
@@ -224,11 +246,13 @@ hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStr
 hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
     if (grid <= 0) grid = default_grid(a.total_tiles, 4);
     if (a.nout <= 4 * 8)
-        hipLaunchKernelGGL((rs_matmul_generic<8, 4>), dim3(grid), dim3(4 * 64), 0, s, a);
+        hipLaunchKernelGGL((rs_matmul_generic<8, 4>), dim3(grid), dim3(4 * 64), (generic_coef_lds_bytes<8, 4>(a)), s, a);
     else if (a.nout <= 4 * 16)
-        hipLaunchKernelGGL((rs_matmul_generic<16, 4>), dim3(grid), dim3(4 * 64), 0, s, a);
+        hipLaunchKernelGGL((rs_matmul_generic<16, 4>), dim3(grid), dim3(4 * 64), (generic_coef_lds_bytes<16, 4>(a)), s,
+                           a);
     else
-        hipLaunchKernelGGL((rs_matmul_generic<16, 8>), dim3(grid), dim3(8 * 64), 0, s, a);
+        hipLaunchKernelGGL((rs_matmul_generic<16, 8>), dim3(grid), dim3(8 * 64), (generic_coef_lds_bytes<16, 8>(a)), s,
+                           a);
     return hipGetLastError();
 }
 
