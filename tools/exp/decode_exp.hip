@@ -13,6 +13,72 @@
 using namespace uplink_ec;
 using namespace uplink_ec::dev;
 
+// The previous product rebuild body (nibble tree over the multiples x*2^b),
+// kept here for the experiment variants below.
+namespace uplink_ec { namespace dev {
+// ------------------------------------------------ runtime-matrix body
+__device__ __forceinline__ void mul2_planes(const uint32_t (&o)[8], uint32_t (&n)[8]) {
+    // v*2 mod 0x11d on bit planes: bit0 <- b7, bit1 <- b0, bit2 <- b1^b7,
+    // bit3 <- b2^b7, bit4 <- b3^b7, bit5 <- b4, bit6 <- b5, bit7 <- b6
+    n[0] = o[7];
+    n[1] = o[0];
+    n[2] = o[1] ^ o[7];
+    n[3] = o[2] ^ o[7];
+    n[4] = o[3] ^ o[7];
+    n[5] = o[4];
+    n[6] = o[5];
+    n[7] = o[6];
+}
+
+// add_nibble<B>(acc, y0..y3, c): acc ^= ((c >> B) & 15) * x on bit planes,
+// y0..y3 = x*2^i (i = 0..3 of this nibble).  A 4-level tree of wave-uniform
+// scalar bit tests picks one of 16 leaves; a leaf pairs the set bits so two
+// multiples cost one v_bitop3 XOR3 per plane (expected 20 VALU per
+// coefficient byte, vs 24 for fixed bit pairs and 32 for one branch per
+// bit).  One asm block per nibble keeps the branches scalar (the compiler's
+// structurizer turned the C++ forms into exec-masked code with extra moves).
+#include "rs_nibble_tree.inc"  // tools/gen/gen_nibble_tree.py
+
+// Runtime-matrix body.  For input share j the multiples x*2^b are formed on
+// the fly (3 XORs each on bit planes), four at a time; every output row then
+// walks the nibble tree of its coefficient byte.  The wave's OPW coefficient
+// bytes of input j sit in LDS (staged once per workgroup, zero-padded) and
+// come in with one broadcast LDS read: no global load, and so no vmcnt wait
+// behind outstanding stores, inside the j loop.  Forms measured in
+// tools/exp/decode_exp.hip (RS(29,80), 64 MiB segments, m = 29 / 17 missing):
+// one branch per bit 83/78 us, fixed bit pairs 71/55, nibble tree 66/52,
+// + LDS coefficients 61.5/47.3.
+template <int OPW>
+__device__ __forceinline__ void compute_generic(const uint32_t *lds, const uint8_t *lcoef, int coef_stride, int lane,
+                                                int jn, int cnt, uint32_t (&acc)[OPW][8]) {
+    static_assert(OPW % 4 == 0, "coefficient slots are whole words");
+    constexpr int NWORD = OPW / 4;
+    for (int jj = 0; jj < jn; jj++) {
+        uint32_t y0[8], y1[8], y2[8], y3[8];
+#pragma unroll
+        for (int p = 0; p < 8; p++) y0[p] = lds[(jj * 8 + p) * 64 + lane];
+        const uint32_t *cp = (const uint32_t *)(lcoef + jj * coef_stride);
+        uint32_t cw[NWORD];
+#pragma unroll
+        for (int q = 0; q < NWORD; q++) cw[q] = (uint32_t)__builtin_amdgcn_readfirstlane(cp[q]);
+        mul2_planes(y0, y1);
+        mul2_planes(y1, y2);
+        mul2_planes(y2, y3);
+        static_for<OPW>([&]<int O>() {
+            if (O < cnt) add_nibble<8 * (O % 4)>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+        });
+        mul2_planes(y3, y0);
+        mul2_planes(y0, y1);
+        mul2_planes(y1, y2);
+        mul2_planes(y2, y3);
+        static_for<OPW>([&]<int O>() {
+            if (O < cnt) add_nibble<8 * (O % 4) + 4>(acc[O], y0, y1, y2, y3, cw[O / 4]);
+        });
+    }
+}
+
+}}  // namespace uplink_ec::dev
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 // acc ^= (bit B of c ? y : 0) ^ (bit B+1 of c ? z : 0) with wave-uniform scalar

@@ -208,65 +208,96 @@ __device__ __forceinline__ void compute_special(const uint32_t *lds, int lane, u
 }
 
 // ------------------------------------------------ runtime-matrix body
-__device__ __forceinline__ void mul2_planes(const uint32_t (&o)[8], uint32_t (&n)[8]) {
-    // v*2 mod 0x11d on bit planes: bit0 <- b7, bit1 <- b0, bit2 <- b1^b7,
-    // bit3 <- b2^b7, bit4 <- b3^b7, bit5 <- b4, bit6 <- b5, bit7 <- b6
-    n[0] = o[7];
-    n[1] = o[0];
-    n[2] = o[1] ^ o[7];
-    n[3] = o[2] ^ o[7];
-    n[4] = o[3] ^ o[7];
-    n[5] = o[4];
-    n[6] = o[5];
-    n[7] = o[6];
-}
+// rs_jump_table.inc (tools/gen/gen_jump_table.py): 256 compile-time leaves,
+// leaf c = "acc[row] ^= c * x" as one v_bitop3 per plane from the 4-plane
+// XOR combinations lo[1..15] / hi[1..15] of the current input x.
+#include "rs_jump_table.inc"
 
-// add_nibble<B>(acc, y0..y3, c): acc ^= ((c >> B) & 15) * x on bit planes,
-// y0..y3 = x*2^i (i = 0..3 of this nibble).  A 4-level tree of wave-uniform
-// scalar bit tests picks one of 16 leaves; a leaf pairs the set bits so two
-// multiples cost one v_bitop3 XOR3 per plane (expected 20 VALU per
-// coefficient byte, vs 24 for fixed bit pairs and 32 for one branch per
-// bit).  One asm block per nibble keeps the branches scalar (the compiler's
-// structurizer turned the C++ forms into exec-masked code with extra moves).
-#include "rs_nibble_tree.inc"
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
-// Runtime-matrix body.  For input share j the multiples x*2^b are formed on
-// the fly (3 XORs each on bit planes), four at a time; every output row then
-// walks the nibble tree of its coefficient byte.  The wave's OPW coefficient
-// bytes of input j sit in LDS (staged once per workgroup, zero-padded) and
-// come in with one broadcast LDS read: no global load, and so no vmcnt wait
-// behind outstanding stores, inside the j loop.  Forms measured in
-// tools/exp/decode_exp.hip (RS(29,80), 64 MiB segments, m = 29 / 17 missing):
-// one branch per bit 83/78 us, fixed bit pairs 71/55, nibble tree 66/52,
-// + LDS coefficients 61.5/47.3.
-template <int OPW>
-__device__ __forceinline__ void compute_generic(const uint32_t *lds, const uint8_t *lcoef, int coef_stride, int lane,
-                                                int jn, int cnt, uint32_t (&acc)[OPW][8]) {
-    static_assert(OPW % 4 == 0, "coefficient slots are whole words");
-    constexpr int NWORD = OPW / 4;
-    for (int jj = 0; jj < jn; jj++) {
-        uint32_t y0[8], y1[8], y2[8], y3[8];
-#pragma unroll
-        for (int p = 0; p < 8; p++) y0[p] = lds[(jj * 8 + p) * 64 + lane];
-        const uint32_t *cp = (const uint32_t *)(lcoef + jj * coef_stride);
-        uint32_t cw[NWORD];
-#pragma unroll
-        for (int q = 0; q < NWORD; q++) cw[q] = (uint32_t)__builtin_amdgcn_readfirstlane(cp[q]);
-        mul2_planes(y0, y1);
-        mul2_planes(y1, y2);
-        mul2_planes(y2, y3);
-        static_for<OPW>([&]<int O>() {
-            if (O < cnt) add_nibble<8 * (O % 4)>(acc[O], y0, y1, y2, y3, cw[O / 4]);
-        });
-        mul2_planes(y3, y0);
-        mul2_planes(y0, y1);
-        mul2_planes(y1, y2);
-        mul2_planes(y2, y3);
-        static_for<OPW>([&]<int O>() {
-            if (O < cnt) add_nibble<8 * (O % 4) + 4>(acc[O], y0, y1, y2, y3, cw[O / 4]);
-        });
-    }
+#define RS_JT_CALL(IDX, EXTRACT)            \
+    "s_set_gpr_idx_idx " #IDX "\n" EXTRACT  \
+    "s_add_u32 s42, s40, s50\n"             \
+    "s_addc_u32 s43, s41, 0\n"              \
+    "s_swappc_b64 s[48:49], s[42:43]\n"
+
+// acc[O] ^= D[row O][j] * x_j for the wave's 8 accumulator rows (rows past the
+// wave's count have coefficient 0 = an empty leaf).  xa = LDS byte address of
+// plane 0 of x_j for this lane (plane p at +256 p); ca = LDS address of the 8
+// 16-bit leaf offsets (coefficient * RS_JT_SLOT) of the wave's rows for j.
+// The planes land directly in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8];
+// 22 XORs fill the other combinations; then, with VGPR index mode on for the
+// accumulator operand (SRC0 and DST, M0 = 8 * row), one s_swappc_b64 per row
+// runs the leaf of its coefficient, which returns with s_setpc_b64.
+// Registers are fixed by the register contract of rs_jump_table.inc: acc in
+// v[32:95] (pinned operands), combinations v[96:125], s[40:51] scratch.
+__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t ca) {
+    asm volatile(
+        "s_mov_b32 s51, m0\n"
+        "ds_read_b32 v96, %[xa]\n"
+        "ds_read_b32 v97, %[xa] offset:256\n"
+        "ds_read_b32 v99, %[xa] offset:512\n"
+        "ds_read_b32 v103, %[xa] offset:768\n"
+        "ds_read_b32 v111, %[xa] offset:1024\n"
+        "ds_read_b32 v112, %[xa] offset:1280\n"
+        "ds_read_b32 v114, %[xa] offset:1536\n"
+        "ds_read_b32 v118, %[xa] offset:1792\n"
+        "ds_read_b128 v[104:107], %[ca]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 s44, v104\n"
+        "v_readfirstlane_b32 s45, v105\n"
+        "v_readfirstlane_b32 s46, v106\n"
+        "v_readfirstlane_b32 s47, v107\n"
+        "v_xor_b32 v98, v96, v97\n"
+        "v_xor_b32 v100, v96, v99\n"
+        "v_xor_b32 v101, v97, v99\n"
+        "v_xor_b32 v102, v98, v99\n"
+        "v_xor_b32 v104, v96, v103\n"
+        "v_xor_b32 v105, v97, v103\n"
+        "v_xor_b32 v106, v98, v103\n"
+        "v_xor_b32 v107, v99, v103\n"
+        "v_xor_b32 v108, v100, v103\n"
+        "v_xor_b32 v109, v101, v103\n"
+        "v_xor_b32 v110, v102, v103\n"
+        "v_xor_b32 v113, v111, v112\n"
+        "v_xor_b32 v115, v111, v114\n"
+        "v_xor_b32 v116, v112, v114\n"
+        "v_xor_b32 v117, v113, v114\n"
+        "v_xor_b32 v119, v111, v118\n"
+        "v_xor_b32 v120, v112, v118\n"
+        "v_xor_b32 v121, v113, v118\n"
+        "v_xor_b32 v122, v114, v118\n"
+        "v_xor_b32 v123, v115, v118\n"
+        "v_xor_b32 v124, v116, v118\n"
+        "v_xor_b32 v125, v117, v118\n"
+        "s_getpc_b64 s[40:41]\n"
+        ".Ljt_pc%=:\n"
+        "s_add_u32 s40, s40, .Ljt_tab%=-.Ljt_pc%=\n"
+        "s_addc_u32 s41, s41, 0\n"
+        "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+        RS_JT_CALL(0, "s_and_b32 s50, s44, 0xffff\n")
+        RS_JT_CALL(8, "s_lshr_b32 s50, s44, 16\n")
+        RS_JT_CALL(16, "s_and_b32 s50, s45, 0xffff\n")
+        RS_JT_CALL(24, "s_lshr_b32 s50, s45, 16\n")
+        RS_JT_CALL(32, "s_and_b32 s50, s46, 0xffff\n")
+        RS_JT_CALL(40, "s_lshr_b32 s50, s46, 16\n")
+        RS_JT_CALL(48, "s_and_b32 s50, s47, 0xffff\n")
+        RS_JT_CALL(56, "s_lshr_b32 s50, s47, 16\n")
+        "s_set_gpr_idx_off\n"
+        "s_mov_b32 m0, s51\n"
+        "s_branch .Ljt_end%=\n"
+        ".Ljt_tab%=:\n"
+        RS_JUMP_TABLE_ASM
+        ".Ljt_end%=:\n"
+        : "+{v[32:39]}"(acc[0]), "+{v[40:47]}"(acc[1]), "+{v[48:55]}"(acc[2]), "+{v[56:63]}"(acc[3]),
+          "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7])
+        : [xa] "v"(xa), [ca] "v"(ca)
+        : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
+          "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
+          "v122", "v123", "v124", "v125", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49",
+          "s50", "s51", "scc", "memory");
 }
+#undef RS_JT_CALL
 
 }  // namespace dev
 }  // namespace uplink_ec

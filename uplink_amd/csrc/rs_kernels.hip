@@ -27,10 +27,11 @@
 //    XOR of two precomputed 4-plane combinations ("four Russians"), one
 //    v_bitop3 per (output plane, input share): 8 ops per GF multiply-add of a
 //    32-byte column block instead of ~16 for the plain bit-matrix.
-//  * rs_matmul_generic<OPW>: any runtime matrix (encode for arbitrary (k,n),
-//    and the rebuild matrix (G_S)^-1 of a share set).  The input's multiples
-//    x*2^b are formed once per input (21 XORs); each coefficient bit pair is
-//    then a wave-uniform branch adding one or two of them.
+//  * rs_matmul_jt<NW>: any runtime matrix (encode for arbitrary (k,n), and
+//    the rebuild matrix (G_S)^-1 of a share set).  Same four-Russians body,
+//    but the coefficient is data: each (row, input) pair is one call into a
+//    table of 256 compile-time leaves (rs_jump_table.inc), the accumulator
+//    row picked by VGPR index mode -- no per-bit branches.
 #include "rs_device.hpp"
 
 namespace uplink_ec {
@@ -97,24 +98,24 @@ __global__ __launch_bounds__(kThreads, 1) void rs_encode_special(const RsArgs a)
 }
 
 // Runtime-matrix kernel (rebuild, and encode for (k, n) without a
-// specialised kernel).  Compute-bound (the decode matrix is data), so every
-// wave computes (no loader waves) and several workgroups share a CU; inputs
-// are staged in LDS chunks of kGenericJC shares.  The rows of a pass are
-// spread evenly over the NW waves (counts differ by at most one, <= OPW) and
-// the row group of a wave is rotated by blockIdx so the SIMDs of a CU, which
-// host waves of several workgroups, get equal VALU work.  The coefficients
-// are copied once per workgroup into dynamic LDS as [pass][j][group][OPW]
-// bytes (zero-padded): generic_coef_lds_bytes() gives the size.
-// 4 waves x 8 rows with 8-share chunks measured fastest (61.5 us at m = 29,
-// 47.3 us at m = 17 per RS(29,80) 64 MiB segment: tools/exp/decode_exp.hip).
-constexpr int kGenericJC = 8;
+// specialised kernel).  Every wave computes (no loader waves) and several
+// workgroups share a CU; inputs are staged in LDS chunks of 2*NW shares.
+// The rows of a pass are spread evenly over the NW waves (<= 8 each, the
+// accumulators of jt_input), each wave stages two inputs of a chunk of 2*NW,
+// and the row group of a wave is rotated by
+// blockIdx so the SIMDs of a CU, which host waves of several workgroups, get
+// equal VALU work.  Each coefficient is multiplied in through the jump table
+// (jt_input): the LDS copy of the matrix holds leaf offsets c * RS_JT_SLOT as
+// [pass][j][group][8] 16-bit words (0 = empty leaf for padded rows), built
+// once per workgroup; jt_lds_bytes() gives the dynamic LDS size.
+constexpr int kJtRows = 8;  // accumulator rows per wave
 
-template <int OPW, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) {
-    constexpr int JC = kGenericJC;
-    constexpr int PER = (JC + NW - 1) / NW;
-    __shared__ uint32_t lds[JC * 8 * 64];
-    extern __shared__ __attribute__((aligned(16))) uint8_t lcoef[];
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
+    constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *lds = smem;                              // [JC][8 planes][64 lanes]
+    uint16_t *lco = (uint16_t *)(smem + JC * 8 * 64);  // leaf offsets
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
@@ -126,10 +127,12 @@ __global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) 
             const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
             const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
             const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
-            lcoef[t] = o < cn ? a.coef[(int64_t)j * a.coef_ld + rb + o] : 0;
+            lco[t] = o < cn ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + o] * RS_JT_SLOT) : (uint16_t)0;
         }
     }
     __syncthreads();
+    const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 4;
+    const uint32_t lco_addr = (uint32_t)(uintptr_t)lco;
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
         const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
@@ -137,29 +140,35 @@ __global__ __launch_bounds__(NW * 64, 2) void rs_matmul_generic(const RsArgs a) 
             const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
             const int rbase = p0 + group * prow / NW;
             const int cnt = p0 + (group + 1) * prow / NW - rbase;
-            uint32_t acc[OPW][8];
+            u32x8 acc[OPW];
 #pragma unroll
-            for (int o = 0; o < OPW; o++)
-#pragma unroll
-                for (int p = 0; p < 8; p++) acc[o][p] = 0;
+            for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
             for (int j0 = 0; j0 < a.nin; j0 += JC) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
                 stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
                 __syncthreads();
-                if (cnt > 0)
-                    compute_generic<OPW>(lds, lcoef + ((pass * a.nin + j0) * NW + group) * OPW, NW * OPW, lane, jn,
-                                         cnt, acc);
+                if (cnt > 0) {
+#pragma nounroll
+                    for (int jj = 0; jj < jn; jj++)
+                        jt_input(acc, lds_addr + (uint32_t)(jj * 8 * 64 * 4),
+                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2));
+                }
                 __syncthreads();
             }
-            store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+            uint32_t rows[OPW][8];
+#pragma unroll
+            for (int o = 0; o < OPW; o++)
+#pragma unroll
+                for (int p = 0; p < 8; p++) rows[o][p] = acc[o][p];
+            store_rows<OPW, true>(a, seg, c, rbase, cnt, rows);
         }
     }
 }
 
-template <int OPW, int NW>
-size_t generic_coef_lds_bytes(const RsArgs &a) {
-    const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
-    return (size_t)npass * a.nin * NW * OPW;
+template <int NW>
+size_t jt_lds_bytes(const RsArgs &a) {
+    const int npass = a.nout > 0 ? (a.nout + NW * kJtRows - 1) / (NW * kJtRows) : 1;
+    return (size_t)2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
 }
 
 // ------------------------------------------------ byte-wise fallback
@@ -244,15 +253,14 @@ hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStr
 }
 
 hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
-    if (grid <= 0) grid = default_grid(a.total_tiles, 4);
-    if (a.nout <= 4 * 8)
-        hipLaunchKernelGGL((rs_matmul_generic<8, 4>), dim3(grid), dim3(4 * 64), (generic_coef_lds_bytes<8, 4>(a)), s, a);
-    else if (a.nout <= 4 * 16)
-        hipLaunchKernelGGL((rs_matmul_generic<16, 4>), dim3(grid), dim3(4 * 64), (generic_coef_lds_bytes<16, 4>(a)), s,
-                           a);
-    else
-        hipLaunchKernelGGL((rs_matmul_generic<16, 8>), dim3(grid), dim3(8 * 64), (generic_coef_lds_bytes<16, 8>(a)), s,
-                           a);
+    // 16 waves per CU (4 per SIMD: the jump-table body holds ~126 VGPRs)
+    if (a.nout <= 2 * kJtRows) {
+        if (grid <= 0) grid = default_grid(a.total_tiles, 8);
+        hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);
+    } else {
+        if (grid <= 0) grid = default_grid(a.total_tiles, 4);
+        hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
+    }
     return hipGetLastError();
 }
 
