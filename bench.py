@@ -52,10 +52,15 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="untimed steps run for at least this long before the W warm-up steps: the chip's clocks "
+                         "ramp for tens of ms under sustained load (DESIGN.md §5)")
     ap.add_argument("--batch", type=int, default=8, help="segments per step per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-segments", type=int, default=4)
+    ap.add_argument("--cpu-sample-s", type=float, default=10.0,
+                    help="CPU baseline: cycle over the sample segments for at least this many seconds")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -81,17 +86,22 @@ def share_sets():
     return sets
 
 
-def cpu_baseline(threads: int, nseg: int):
+def cpu_baseline(threads: int, nseg: int, min_s: float):
     """Reference-shaped CPU loops of the oracle (per piece per stripe
     EncodeSingle, per stripe Rebuild with its k x k inversion) on `nseg`
-    segments: test infrastructure used only for this reported baseline."""
+    distinct segments, cycled until `min_s` seconds of CPU work: test
+    infrastructure used only for this reported baseline."""
     from oracle import oracle as O
     f = O.FEC(K, N)
     rng = np.random.default_rng(7)
     segs = [np.frombuffer(rng.bytes(S_PAD), dtype=np.uint8) for _ in range(nseg)]
     sets = share_sets()
     t_enc = t_dec = 0.0
-    for i, seg in enumerate(segs):
+    done = 0
+    while done < nseg or t_enc + t_dec < min_s:
+        i = done
+        seg = segs[i % nseg]
+        done += 1
         t0 = time.perf_counter()
         pieces = f.encode_segment(seg, ESS, threads=threads)
         t1 = time.perf_counter()
@@ -101,13 +111,14 @@ def cpu_baseline(threads: int, nseg: int):
         assert np.array_equal(out, seg)
         t_enc += t1 - t0
         t_dec += t2 - t1
-    gib = nseg * S_PAD / 2**30
+    gib = done * S_PAD / 2**30
     return {
         "value": round(gib / (t_enc + t_dec), 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{nseg} x 64 MiB RS(29,80) segments: oracle reference-shaped encode (EncodeSingle per piece "
+        "sample": f"{done} x 64 MiB RS(29,80) segments ({nseg} distinct, cycled): oracle reference-shaped encode "
+                  f"(EncodeSingle per piece "
                   f"per stripe, AVX2 PSHUFB addmul) + per-stripe Rebuild from the same 29-piece sets as the GPU run; "
                   f"encode {t_enc:.3f}s, decode {t_dec:.3f}s wall on {threads} threads",
         "encode_gibps": round(gib / t_enc, 4),
@@ -170,6 +181,14 @@ def main():
     for s in range(len(sets)):
         encode()
         decode(s)
+    t_settle = time.perf_counter()
+    s = 0
+    while time.perf_counter() - t_settle < args.settle_s:
+        encode()
+        decode(s)
+        s += 1
+        if s % 8 == 0:
+            torch.cuda.synchronize(dev)
     for s in range(args.warmup):
         encode()
         decode(s)
@@ -253,7 +272,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(os.cpu_count() or 1, 16)
-        line["cpu_baseline"] = cpu_baseline(threads, args.cpu_sample_segments)
+        line["cpu_baseline"] = cpu_baseline(threads, args.cpu_sample_segments, args.cpu_sample_s)
     if rank == 0:
         print(json.dumps(line), flush=True)
     L.ec_destroy(ctx)

@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "../../uplink_amd/csrc/rs_device.hpp"
-#include "../../uplink_amd/csrc/rs_jump_table.inc"
+#include "rs_jump_table_exp.inc"
 
 using namespace uplink_ec;
 using namespace uplink_ec::dev;
@@ -28,99 +28,7 @@ using namespace uplink_ec::dev;
 
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
-#if defined(JT_NOJUMP)
-#define JT_LEAF_P(P) "v_bitop3_b32 v" #P ", v" #P ", v" #P ", v" #P " bitop3:0x96\n"
-#define JT_CALL(IDX, EXTRACT)                 \
-    "s_set_gpr_idx_idx " #IDX "\n" EXTRACT    \
-    "s_add_u32 s42, s40, s50\n"               \
-    "s_addc_u32 s43, s41, 0\n"                \
-    JT_NJ_LEAF
-#elif defined(JT_FIXEDTGT)
-#define JT_CALL(IDX, EXTRACT)                 \
-    "s_set_gpr_idx_idx " #IDX "\n"            \
-    "s_swappc_b64 s[48:49], s[42:43]\n"
-#else
-#define JT_CALL(IDX, EXTRACT)                 \
-    "s_set_gpr_idx_idx " #IDX "\n" EXTRACT    \
-    "s_add_u32 s42, s40, s50\n"               \
-    "s_addc_u32 s43, s41, 0\n"                \
-    "s_swappc_b64 s[48:49], s[42:43]\n"
-#endif
-
-// acc rows 0..7 (+= D[row][j] * x_j) for one input whose 8 planes are at LDS
-// byte address xa (+256 per plane); ca = LDS address of the 8 16-bit leaf
-// offsets (coefficient * RS_JT_SLOT) of this wave's rows.
-__device__ __forceinline__ void jt_input_x(u32x8 (&acc)[8], uint32_t xa, uint32_t ca) {
-    asm volatile(
-        "s_mov_b32 s51, m0\n"
-        "ds_read_b32 v96, %[xa]\n"
-        "ds_read_b32 v97, %[xa] offset:256\n"
-        "ds_read_b32 v99, %[xa] offset:512\n"
-        "ds_read_b32 v103, %[xa] offset:768\n"
-        "ds_read_b32 v111, %[xa] offset:1024\n"
-        "ds_read_b32 v112, %[xa] offset:1280\n"
-        "ds_read_b32 v114, %[xa] offset:1536\n"
-        "ds_read_b32 v118, %[xa] offset:1792\n"
-        "ds_read_b128 v[104:107], %[ca]\n"
-        "s_waitcnt lgkmcnt(0)\n"
-        "v_readfirstlane_b32 s44, v104\n"
-        "v_readfirstlane_b32 s45, v105\n"
-        "v_readfirstlane_b32 s46, v106\n"
-        "v_readfirstlane_b32 s47, v107\n"
-        "v_xor_b32 v98, v96, v97\n"
-        "v_xor_b32 v100, v96, v99\n"
-        "v_xor_b32 v101, v97, v99\n"
-        "v_xor_b32 v102, v98, v99\n"
-        "v_xor_b32 v104, v96, v103\n"
-        "v_xor_b32 v105, v97, v103\n"
-        "v_xor_b32 v106, v98, v103\n"
-        "v_xor_b32 v107, v99, v103\n"
-        "v_xor_b32 v108, v100, v103\n"
-        "v_xor_b32 v109, v101, v103\n"
-        "v_xor_b32 v110, v102, v103\n"
-        "v_xor_b32 v113, v111, v112\n"
-        "v_xor_b32 v115, v111, v114\n"
-        "v_xor_b32 v116, v112, v114\n"
-        "v_xor_b32 v117, v113, v114\n"
-        "v_xor_b32 v119, v111, v118\n"
-        "v_xor_b32 v120, v112, v118\n"
-        "v_xor_b32 v121, v113, v118\n"
-        "v_xor_b32 v122, v114, v118\n"
-        "v_xor_b32 v123, v115, v118\n"
-        "v_xor_b32 v124, v116, v118\n"
-        "v_xor_b32 v125, v117, v118\n"
-        "s_getpc_b64 s[40:41]\n"
-        ".Lgp%=:\n"
-        "s_add_u32 s40, s40, .Ltab%=-.Lgp%=\n"
-        "s_addc_u32 s41, s41, 0\n"
-#ifdef JT_FIXEDTGT
-        "s_and_b32 s50, s44, 0xffff\n"
-        "s_add_u32 s42, s40, s50\n"
-        "s_addc_u32 s43, s41, 0\n"
-#endif
-        "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-        JT_CALL(0, "s_and_b32 s50, s44, 0xffff\n")
-        JT_CALL(8, "s_lshr_b32 s50, s44, 16\n")
-        JT_CALL(16, "s_and_b32 s50, s45, 0xffff\n")
-        JT_CALL(24, "s_lshr_b32 s50, s45, 16\n")
-        JT_CALL(32, "s_and_b32 s50, s46, 0xffff\n")
-        JT_CALL(40, "s_lshr_b32 s50, s46, 16\n")
-        JT_CALL(48, "s_and_b32 s50, s47, 0xffff\n")
-        JT_CALL(56, "s_lshr_b32 s50, s47, 16\n")
-        "s_set_gpr_idx_off\n"
-        "s_mov_b32 m0, s51\n"
-        "s_branch .Lend%=\n"
-        ".Ltab%=:\n"
-        RS_JUMP_TABLE_ASM
-        ".Lend%=:\n"
-        : "+{v[32:39]}"(acc[0]), "+{v[40:47]}"(acc[1]), "+{v[48:55]}"(acc[2]), "+{v[56:63]}"(acc[3]),
-          "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7])
-        : [xa] "v"(xa), [ca] "v"(ca)
-        : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
-          "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
-          "v122", "v123", "v124", "v125", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49",
-          "s50", "s51", "scc", "memory");
-}
+#include "jt_chunk_exp.inc"
 
 constexpr int JC = 8;
 
@@ -143,7 +51,8 @@ __global__ __launch_bounds__(NW * 64, MINW) void dec_jt(const RsArgs a) {
             const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
             const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
             const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
-            lco[t] = o < cn ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + o] * RS_JT_SLOT) : 0;
+            const int oo = o - (OPW - cn);  // rows right-aligned: slot OPW-cn+i holds row i
+            lco[t] = oo >= 0 ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + oo] * RS_JT_SLOT) : 0;
         }
     }
     __syncthreads();
@@ -165,12 +74,9 @@ __global__ __launch_bounds__(NW * 64, MINW) void dec_jt(const RsArgs a) {
                 else for (int q = threadIdx.x; q < jn * 8 * 64; q += NW * 64) lds[q] = q * 0x9E3779B9u + (uint32_t)tile;
                 __syncthreads();
                 if (MODE != 1 && cnt > 0) {
-#pragma nounroll
-                    for (int jj = 0; jj < jn; jj++) {
-                        const uint32_t xa = lds_base + (uint32_t)((jj * 8 * 64 + lane) * 4);
-                        const uint32_t ca = lco_base + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2);
-                        jt_input_x(acc, xa, ca);
-                    }
+                    jt_chunk<NW>(acc, lds_base + (uint32_t)(lane * 4),
+                             lco_base + (uint32_t)((((pass * a.nin + j0) * NW + group) * OPW) * 2), (uint32_t)jn,
+                             (uint32_t)(OPW - cnt));
                 }
                 __syncthreads();
             }

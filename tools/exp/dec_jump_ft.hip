@@ -57,7 +57,7 @@ typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 // acc rows 0..7 (+= D[row][j] * x_j) for one input whose 8 planes are at LDS
 // byte address xa (+256 per plane); ca = LDS address of the 8 16-bit leaf
 // offsets (coefficient * RS_JT_SLOT) of this wave's rows.
-__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t ca) {
+__device__ __forceinline__ void jt_input_x(u32x8 (&acc)[8], uint32_t xa, uint32_t ca) {
     asm volatile(
         "s_mov_b32 s51, m0\n"
         "ds_read_b32 v96, %[xa]\n"
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(NW * 64, MINW) void dec_jt(const RsArgs a) {
                     for (int jj = 0; jj < jn; jj++) {
                         const uint32_t xa = lds_base + (uint32_t)((jj * 8 * 64 + lane) * 4);
                         const uint32_t ca = lco_base + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2);
-                        jt_input(acc, xa, ca);
+                        jt_input_x(acc, xa, ca);
                     }
                 }
                 __syncthreads();

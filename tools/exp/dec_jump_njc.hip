@@ -1,3 +1,5 @@
+#define JT_NOJUMP 1
+#define JT_NJ_LEAF "v_bitop3_b32 v32, v32, v97, v112 bitop3:0x96\n" "v_bitop3_b32 v33, v33, v98, v113 bitop3:0x96\n" "v_bitop3_b32 v34, v34, v99, v114 bitop3:0x96\n" "v_bitop3_b32 v35, v35, v100, v115 bitop3:0x96\n" "v_bitop3_b32 v36, v36, v101, v116 bitop3:0x96\n" "v_bitop3_b32 v37, v37, v102, v117 bitop3:0x96\n" "v_bitop3_b32 v38, v38, v103, v118 bitop3:0x96\n" "v_bitop3_b32 v39, v39, v104, v119 bitop3:0x96\n"
 // Developer experiment (not product): rebuild body that multiplies by a
 // runtime coefficient through a jump table of 256 compile-time leaves
 // (tools/gen/gen_jump_table.py), the accumulator row chosen by VGPR index
