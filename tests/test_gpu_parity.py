@@ -388,3 +388,33 @@ def test_host_pipeline_encode_rebuild(oracle):
     finally:
         for p in (ps, pp, po):
             lib.ec_host_free(p)
+
+
+def test_c1_loopback_piecestore(oracle):
+    """BASELINE configs[0] / SURVEY §8d C1: RS(4,10), ess 256, a 1 MiB
+    segment through the upload path (PadReader, one EncodedReader per piece,
+    segmentupload/encode.go:16-75) into an in-process piece store (the
+    MockPieceStore role, piecestore/client_test.go:136-179), then downloaded
+    from pieces {6,7,8,9} and from a seeded random 4-subset (Rebuild over all
+    stripes, stripe.go:382-428) and unpadded."""
+    import io
+    k, n, ess = 4, 10, 256
+    rs = eestream.RedundancyStrategy(scheme(k, n, ess), 0, 0)
+    data = np.random.default_rng(20261015).integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+    padded = eestream.pad(data, rs.stripe_size())
+    stripes = len(padded) // rs.stripe_size()
+    assert stripes == 1025
+    store = {}
+    for num in range(n):
+        piece = eestream.new_encoded_reader(io.BytesIO(padded), rs, num).read()
+        assert len(piece) == eestream.calc_piece_size(len(data), rs)
+        store[num] = piece
+    ref = oracle.FEC(k, n).encode_segment(np.frombuffer(padded, dtype=np.uint8), ess)
+    for num in range(n):
+        assert np.array_equal(np.frombuffer(store[num], dtype=np.uint8), ref[num])
+    d_pieces = torch.from_numpy(np.stack([np.frombuffer(store[i], dtype=np.uint8) for i in range(n)])).cuda()
+    d_pieces = d_pieces.reshape(1, n, -1)
+    rng = np.random.default_rng(4)
+    for nums in ([6, 7, 8, 9], sorted(rng.choice(n, k, replace=False).tolist())):
+        out = gpu_rebuild(rs.scheme, d_pieces, nums, stripes)[0]
+        assert eestream.unpad(out.tobytes()) == data
