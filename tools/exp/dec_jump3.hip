@@ -176,6 +176,70 @@ size_t dma_lds_bytes(const RsArgs &a) {
     return (size_t)PER * NW * (2048 + 2048) + (size_t)npass * a.nin * NW * 8 * 2;
 }
 
+constexpr int kJtRows = 8;  // accumulator rows per wave
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
+    constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *lds = smem;                              // [JC][8 planes][64 lanes]
+    uint16_t *lco = (uint16_t *)(smem + JC * 8 * 64);  // leaf offsets
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
+    const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
+    {
+        const int per_pass = a.nin * NW * OPW;
+        for (int t = threadIdx.x; t < npass * per_pass; t += NW * 64) {
+            const int pass = t / per_pass, r = t - pass * per_pass;
+            const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
+            const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
+            const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
+            lco[t] = o < cn ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + o] * RS_JT_SLOT) : (uint16_t)0;
+        }
+    }
+    __syncthreads();
+    const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 4;
+    const uint32_t lco_addr = (uint32_t)(uintptr_t)lco;
+    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const int64_t seg = tile / a.tiles_per_seg;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        for (int pass = 0; pass < npass; pass++) {
+            const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
+            const int rbase = p0 + group * prow / NW;
+            const int cnt = p0 + (group + 1) * prow / NW - rbase;
+            u32x8 acc[OPW];
+#pragma unroll
+            for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
+            for (int j0 = 0; j0 < a.nin; j0 += JC) {
+                const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+                stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
+                __syncthreads();
+                if (cnt > 0) {
+#pragma nounroll
+                    for (int jj = 0; jj < jn; jj++)
+                        jt_input(acc, lds_addr + (uint32_t)(jj * 8 * 64 * 4),
+                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2));
+                }
+                __syncthreads();
+            }
+            uint32_t rows[OPW][8];
+#pragma unroll
+            for (int o = 0; o < OPW; o++)
+#pragma unroll
+                for (int p = 0; p < 8; p++) rows[o][p] = acc[o][p];
+            store_rows<OPW, true>(a, seg, c, rbase, cnt, rows);
+        }
+    }
+}
+
+template <int NW>
+size_t jt_lds_bytes(const RsArgs &a) {
+    const int npass = a.nout > 0 ? (a.nout + NW * kJtRows - 1) / (NW * kJtRows) : 1;
+    return (size_t)2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
+}
+
+
 int main(int argc, char **argv) {
     const int only = argc > 1 ? atoi(argv[1]) : -1;
     int vidx = 0;
@@ -298,8 +362,8 @@ int main(int argc, char **argv) {
         const size_t sh2 = dma_lds_bytes<4, 2>(a), sh4 = dma_lds_bytes<4, 4>(a), sh3 = dma_lds_bytes<4, 3>(a);
         for (int rep = 0; rep < 2; rep++) {
             timeit("dma NW4 JC8 grid4x", sh2, [&](size_t sh) { hipLaunchKernelGGL((dec_dma<4, 2>), dim3(cus * 4), dim3(256), sh, 0, a); });
-            timeit("dma NW4 JC12 grid4x", sh3, [&](size_t sh) { hipLaunchKernelGGL((dec_dma<4, 3>), dim3(cus * 4), dim3(256), sh, 0, a); });
-            timeit("dma NW4 JC16 grid4x", sh4, [&](size_t sh) { hipLaunchKernelGGL((dec_dma<4, 4>), dim3(cus * 4), dim3(256), sh, 0, a); });
+            timeit("product jt NW4 grid4x", jt_lds_bytes<4>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(cus * 4), dim3(256), sh, 0, a); });
+            if (R <= 16) timeit("product jt NW2 grid8x", jt_lds_bytes<2>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(cus * 8), dim3(128), sh, 0, a); });
         }
     }
     return 0;

@@ -215,22 +215,17 @@ __device__ __forceinline__ void compute_special(const uint32_t *lds, int lane, u
 
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
-#define RS_JT_CALL(IDX, EXTRACT)            \
-    "s_set_gpr_idx_idx " #IDX "\n" EXTRACT  \
-    "s_add_u32 s42, s40, s50\n"             \
-    "s_addc_u32 s43, s41, 0\n"              \
-    "s_swappc_b64 s[48:49], s[42:43]\n"
-
 // acc[O] ^= D[row O][j] * x_j for the wave's 8 accumulator rows (rows past the
 // wave's count have coefficient 0 = an empty leaf).  xa = LDS byte address of
 // plane 0 of x_j for this lane (plane p at +256 p); ca = LDS address of the 8
 // 16-bit leaf offsets (coefficient * RS_JT_SLOT) of the wave's rows for j.
 // The planes land directly in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8];
-// 22 XORs fill the other combinations; then, with VGPR index mode on for the
-// accumulator operand (SRC0 and DST, M0 = 8 * row), one s_swappc_b64 per row
-// runs the leaf of its coefficient, which returns with s_setpc_b64.
+// 22 XORs fill the other combinations; the 8 leaf addresses are formed up
+// front (s[52:67]); then, with VGPR index mode on for the accumulator operand
+// (SRC0 and DST, M0 = 8 * row, stepped by each leaf), eight back-to-back
+// s_swappc_b64 run the leaves, which return with s_setpc_b64.
 // Registers are fixed by the register contract of rs_jump_table.inc: acc in
-// v[32:95] (pinned operands), combinations v[96:125], s[40:51] scratch.
+// v[32:95] (pinned operands), combinations v[96:125], s[40:67] scratch.
 __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t ca) {
     asm volatile(
         "s_mov_b32 s51, m0\n"
@@ -243,6 +238,10 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         "ds_read_b32 v114, %[xa] offset:1536\n"
         "ds_read_b32 v118, %[xa] offset:1792\n"
         "ds_read_b128 v[104:107], %[ca]\n"
+        "s_getpc_b64 s[40:41]\n"
+        ".Ljt_pc%=:\n"
+        "s_add_u32 s40, s40, .Ljt_tab%=-.Ljt_pc%=\n"
+        "s_addc_u32 s41, s41, 0\n"
         "s_waitcnt lgkmcnt(0)\n"
         "v_readfirstlane_b32 s44, v104\n"
         "v_readfirstlane_b32 s45, v105\n"
@@ -270,19 +269,39 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         "v_xor_b32 v123, v115, v118\n"
         "v_xor_b32 v124, v116, v118\n"
         "v_xor_b32 v125, v117, v118\n"
-        "s_getpc_b64 s[40:41]\n"
-        ".Ljt_pc%=:\n"
-        "s_add_u32 s40, s40, .Ljt_tab%=-.Ljt_pc%=\n"
-        "s_addc_u32 s41, s41, 0\n"
+        "s_and_b32 s50, s44, 0xffff\n"
+        "s_add_u32 s52, s40, s50\n"
+        "s_addc_u32 s53, s41, 0\n"
+        "s_lshr_b32 s50, s44, 16\n"
+        "s_add_u32 s54, s40, s50\n"
+        "s_addc_u32 s55, s41, 0\n"
+        "s_and_b32 s50, s45, 0xffff\n"
+        "s_add_u32 s56, s40, s50\n"
+        "s_addc_u32 s57, s41, 0\n"
+        "s_lshr_b32 s50, s45, 16\n"
+        "s_add_u32 s58, s40, s50\n"
+        "s_addc_u32 s59, s41, 0\n"
+        "s_and_b32 s50, s46, 0xffff\n"
+        "s_add_u32 s60, s40, s50\n"
+        "s_addc_u32 s61, s41, 0\n"
+        "s_lshr_b32 s50, s46, 16\n"
+        "s_add_u32 s62, s40, s50\n"
+        "s_addc_u32 s63, s41, 0\n"
+        "s_and_b32 s50, s47, 0xffff\n"
+        "s_add_u32 s64, s40, s50\n"
+        "s_addc_u32 s65, s41, 0\n"
+        "s_lshr_b32 s50, s47, 16\n"
+        "s_add_u32 s66, s40, s50\n"
+        "s_addc_u32 s67, s41, 0\n"
         "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
-        RS_JT_CALL(0, "s_and_b32 s50, s44, 0xffff\n")
-        RS_JT_CALL(8, "s_lshr_b32 s50, s44, 16\n")
-        RS_JT_CALL(16, "s_and_b32 s50, s45, 0xffff\n")
-        RS_JT_CALL(24, "s_lshr_b32 s50, s45, 16\n")
-        RS_JT_CALL(32, "s_and_b32 s50, s46, 0xffff\n")
-        RS_JT_CALL(40, "s_lshr_b32 s50, s46, 16\n")
-        RS_JT_CALL(48, "s_and_b32 s50, s47, 0xffff\n")
-        RS_JT_CALL(56, "s_lshr_b32 s50, s47, 16\n")
+        "s_swappc_b64 s[48:49], s[52:53]\n"
+        "s_swappc_b64 s[48:49], s[54:55]\n"
+        "s_swappc_b64 s[48:49], s[56:57]\n"
+        "s_swappc_b64 s[48:49], s[58:59]\n"
+        "s_swappc_b64 s[48:49], s[60:61]\n"
+        "s_swappc_b64 s[48:49], s[62:63]\n"
+        "s_swappc_b64 s[48:49], s[64:65]\n"
+        "s_swappc_b64 s[48:49], s[66:67]\n"
         "s_set_gpr_idx_off\n"
         "s_mov_b32 m0, s51\n"
         "s_branch .Ljt_end%=\n"
@@ -294,10 +313,10 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         : [xa] "v"(xa), [ca] "v"(ca)
         : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
           "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
-          "v122", "v123", "v124", "v125", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49",
-          "s50", "s51", "scc", "memory");
+          "v122", "v123", "v124", "v125", "s40", "s41", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51",
+          "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
+          "s67", "scc", "memory");
 }
-#undef RS_JT_CALL
 
 }  // namespace dev
 }  // namespace uplink_ec

@@ -114,8 +114,8 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *lds = smem;                              // [JC][8 planes][64 lanes]
-    uint16_t *lco = (uint16_t *)(smem + JC * 8 * 64);  // leaf offsets
+    uint32_t *lds = smem;                                  // 2 x [JC][8 planes][64 lanes]
+    uint16_t *lco = (uint16_t *)(smem + 2 * JC * 8 * 64);  // leaf offsets
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
@@ -133,6 +133,10 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     __syncthreads();
     const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 4;
     const uint32_t lco_addr = (uint32_t)(uintptr_t)lco;
+    // Plane chunks alternate between two LDS buffers, so one barrier per chunk
+    // suffices: a wave staging chunk c+1 has passed barrier c, which every wave
+    // reached only after it finished reading chunk c-1 from that buffer.
+    int buf = 0;
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
         const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
@@ -145,15 +149,15 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
             for (int j0 = 0; j0 < a.nin; j0 += JC) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
-                stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
-                __syncthreads();
+                stage_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0);
+                lds_barrier();
                 if (cnt > 0) {
 #pragma nounroll
                     for (int jj = 0; jj < jn; jj++)
-                        jt_input(acc, lds_addr + (uint32_t)(jj * 8 * 64 * 4),
+                        jt_input(acc, lds_addr + (uint32_t)((buf * JC + jj) * 8 * 64 * 4),
                                  lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2));
                 }
-                __syncthreads();
+                buf ^= 1;
             }
             uint32_t rows[OPW][8];
 #pragma unroll
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 template <int NW>
 size_t jt_lds_bytes(const RsArgs &a) {
     const int npass = a.nout > 0 ? (a.nout + NW * kJtRows - 1) / (NW * kJtRows) : 1;
-    return (size_t)2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
+    return (size_t)2 * 2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
 }
 
 // ------------------------------------------------ byte-wise fallback
