@@ -12,6 +12,8 @@ parity tests read like the reference's own tests:
   calc_piece_size                CalcPieceSize                 encode.go:272-281
   EncodedReader                  segmentupload.EncodedReader   segmentupload/encode.go:16-75
   pad / unpad                    encryption.PadReader/Unpad    (storj.io/common)
+  RSScheme.encode_stripes / .rebuild_stripes
+                                 host-memory batch forms used by streams.py
   SegmentCodec                   batch forms of the per-(piece, stripe) EncodeSingle loop
                                  (segmentupload/single.go:228-238) and of the per-stripe
                                  Rebuild loop (stripe.go:382-428) on device-resident buffers
@@ -227,6 +229,37 @@ class RSScheme:
         _raise(self._ctx, rc)
         dst[:] = tmp[:need]
         return dst
+
+
+    # -- batch forms used by the stream layer (streams.py): whole runs of
+    #    stripes per engine call instead of one call per (piece, stripe)
+    def encode_stripes(self, data) -> np.ndarray:
+        """EncodeSingle for every piece of len(data)/StripeSize stripes:
+        returns [n][stripes*ess] (host memory in and out)."""
+        a = _u8(data)
+        stripe = self.stripe_size()
+        if a.size % stripe:
+            _raise(self._ctx, N.EC_ERR_INPUT_LENGTH)
+        m = a.size // stripe
+        out = np.empty((self.fc.n, m * self.ess), dtype=np.uint8)
+        if m:
+            _raise(self._ctx, self._lib.ec_encode_segments_host(self._ctx, _ptr(a), 1, m, _ptr(out), 0))
+        return out
+
+    def rebuild_stripes(self, nums, pieces, nstripes: int) -> np.ndarray:
+        """Rebuild over `nstripes` stripes at once from the shares of pieces
+        `nums` (each nstripes*ess host bytes): infectious' share choice, one
+        decode matrix for the run; returns the stripes (nstripes*k*ess)."""
+        arrs = [np.ascontiguousarray(p, dtype=np.uint8) for p in pieces]
+        if len(arrs) != len(nums):
+            raise ValueError("nums and pieces differ in length")
+        out = np.empty(max(nstripes * self.fc.k * self.ess, 1), dtype=np.uint8)
+        c_nums = (ctypes.c_int * max(len(nums), 1))(*nums)
+        c_ptrs = (ctypes.c_void_p * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+        if nstripes:
+            _raise(self._ctx, self._lib.ec_rebuild_segments_host(self._ctx, len(nums), c_nums, c_ptrs, nstripes, 1, 0,
+                                                                 _ptr(out)))
+        return out[:nstripes * self.fc.k * self.ess]
 
 
 def new_rs_scheme(fc: FEC, erasure_share_size: int) -> RSScheme:
