@@ -215,18 +215,19 @@ __device__ __forceinline__ void compute_special(const uint32_t *lds, int lane, u
 
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
-// acc[O] ^= D[row O][j] * x_j for the wave's 8 accumulator rows (rows past the
-// wave's count have coefficient 0 = an empty leaf).  xa = LDS byte address of
-// plane 0 of x_j for this lane (plane p at +256 p); ca = LDS address of the 8
-// 16-bit leaf offsets (coefficient * RS_JT_SLOT) of the wave's rows for j.
+// acc[O] ^= D[row O][j] * x_j for the wave's 8 - skip accumulator rows.
+// xa = LDS byte address of plane 0 of x_j for this lane (plane p at +256 p);
+// ca = LDS address of the 8 16-bit leaf offsets (coefficient * RS_JT_SLOT)
+// of the wave's rows for j, right-aligned (slot skip + i holds row i).
 // The planes land directly in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8];
 // 22 XORs fill the other combinations; the 8 leaf addresses are formed up
 // front (s[52:67]); then, with VGPR index mode on for the accumulator operand
-// (SRC0 and DST, M0 = 8 * row, stepped by each leaf), eight back-to-back
-// s_swappc_b64 run the leaves, which return with s_setpc_b64.
+// (SRC0 and DST, M0 = 8 * row, stepped by each leaf), a jump enters the
+// sequence of eight s_swappc_b64 (4 bytes each) at call site `skip`, so only
+// the wave's rows are visited; the leaves return with s_setpc_b64.
 // Registers are fixed by the register contract of rs_jump_table.inc: acc in
 // v[32:95] (pinned operands), combinations v[96:125], s[40:67] scratch.
-__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t ca) {
+__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t ca, uint32_t skip) {
     asm volatile(
         "s_mov_b32 s51, m0\n"
         "ds_read_b32 v96, %[xa]\n"
@@ -293,7 +294,16 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         "s_lshr_b32 s50, s47, 16\n"
         "s_add_u32 s66, s40, s50\n"
         "s_addc_u32 s67, s41, 0\n"
+        "s_getpc_b64 s[42:43]\n"
+        ".Ljt_pc2%=:\n"
+        "s_lshl_b32 s50, %[skip], 2\n"
+        "s_add_u32 s42, s42, s50\n"
+        "s_addc_u32 s43, s43, 0\n"
+        "s_add_u32 s42, s42, .Ljt_sites%=-.Ljt_pc2%=\n"
+        "s_addc_u32 s43, s43, 0\n"
         "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
+        "s_setpc_b64 s[42:43]\n"
+        ".Ljt_sites%=:\n"
         "s_swappc_b64 s[48:49], s[52:53]\n"
         "s_swappc_b64 s[48:49], s[54:55]\n"
         "s_swappc_b64 s[48:49], s[56:57]\n"
@@ -310,10 +320,10 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         ".Ljt_end%=:\n"
         : "+{v[32:39]}"(acc[0]), "+{v[40:47]}"(acc[1]), "+{v[48:55]}"(acc[2]), "+{v[56:63]}"(acc[3]),
           "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7])
-        : [xa] "v"(xa), [ca] "v"(ca)
+        : [xa] "v"(xa), [ca] "v"(ca), [skip] "s"(skip)
         : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
           "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
-          "v122", "v123", "v124", "v125", "s40", "s41", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51",
+          "v122", "v123", "v124", "v125", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51",
           "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
           "s67", "scc", "memory");
 }

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
             const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
             const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
-            lco[t] = o < cn ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + o] * RS_JT_SLOT) : (uint16_t)0;
+            const int oo = o - (OPW - cn);  // rows right-aligned: jt_input enters at call site OPW - cnt
+            lco[t] = oo >= 0 ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + oo] * RS_JT_SLOT) : (uint16_t)0;
         }
     }
     __syncthreads();
@@ -155,7 +156,8 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 #pragma nounroll
                     for (int jj = 0; jj < jn; jj++)
                         jt_input(acc, lds_addr + (uint32_t)((buf * JC + jj) * 8 * 64 * 4),
-                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2));
+                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2),
+                                 (uint32_t)(OPW - cnt));
                 }
                 buf ^= 1;
             }
@@ -257,10 +259,15 @@ hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStr
 }
 
 hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
-    // 16 waves per CU (4 per SIMD: the jump-table body holds ~126 VGPRs)
+    // up to 16 waves per CU (4 per SIMD: the jump-table body holds ~126
+    // VGPRs); as few waves per workgroup as the rows need, since every wave
+    // rebuilds the 4-plane combinations of each input for its own rows
     if (a.nout <= 2 * kJtRows) {
         if (grid <= 0) grid = default_grid(a.total_tiles, 8);
         hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);
+    } else if (a.nout <= 3 * kJtRows) {
+        if (grid <= 0) grid = default_grid(a.total_tiles, 5);
+        hipLaunchKernelGGL((rs_matmul_jt<3>), dim3(grid), dim3(3 * 64), jt_lds_bytes<3>(a), s, a);
     } else {
         if (grid <= 0) grid = default_grid(a.total_tiles, 4);
         hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
