@@ -209,6 +209,9 @@ def main():
 
     t_enc = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps * 1e-3  # s per launch
     t_dec = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps * 1e-3
+    by_set = {}
+    for st in range(args.steps):
+        by_set.setdefault(st % len(sets), []).append(ev[st][1].elapsed_time(ev[st][2]) * 1e3 / B)
     if world > 1:
         import torch.distributed as dist
         tw = torch.tensor([wall], dtype=torch.float64, device=dev)
@@ -232,8 +235,11 @@ def main():
     kernels = {
         "encode": {"kernel": "rs_encode_special<29,80>", "avg_us": round(t_enc * 1e6, 2),
                    "bytes_per_launch": int(enc_bytes), "achieved_GBps": round(enc_gbps, 1)},
-        "decode": {"kernel": "rs_matmul_jt<4>", "avg_us": round(t_dec * 1e6, 2),
-                   "bytes_per_launch": int(dec_bytes), "achieved_GBps": round(dec_gbps, 1)},
+        "decode": {"kernel": "rs_matmul_jt<NW>", "avg_us": round(t_dec * 1e6, 2),
+                   "bytes_per_launch": int(dec_bytes), "achieved_GBps": round(dec_gbps, 1),
+                   "us_per_segment_by_set": {
+                       f"set{i}:m={K - sum(1 for x in sets[i] if x < K)}": round(sum(v) / len(v), 2)
+                       for i, v in sorted(by_set.items())}},
     }
     dominant = "encode" if t_enc >= t_dec else "decode"
     dk = kernels[dominant]

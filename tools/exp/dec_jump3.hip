@@ -142,7 +142,7 @@ __global__ __launch_bounds__(NW * 64, 4) void dec_dma(const RsArgs a) {
 #pragma nounroll
             for (int jj = 0; jj < jn; jj++)
                 jt_input(acc, pl_addr + (uint32_t)(jj * 8 * 64 * 4),
-                         lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2));
+                         lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2), 0u);
         }
         if (ch == nch - 1) {
             uint32_t rows[OPW][8];
@@ -182,8 +182,8 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t *lds = smem;                              // [JC][8 planes][64 lanes]
-    uint16_t *lco = (uint16_t *)(smem + JC * 8 * 64);  // leaf offsets
+    uint32_t *lds = smem;                                  // 2 x [JC][8 planes][64 lanes]
+    uint16_t *lco = (uint16_t *)(smem + 2 * JC * 8 * 64);  // leaf offsets
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
@@ -195,12 +195,17 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
             const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
             const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
-            lco[t] = o < cn ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + o] * RS_JT_SLOT) : (uint16_t)0;
+            const int oo = o - (OPW - cn);  // rows right-aligned: jt_input enters at call site OPW - cnt
+            lco[t] = oo >= 0 ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + oo] * RS_JT_SLOT) : (uint16_t)0;
         }
     }
     __syncthreads();
     const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 4;
     const uint32_t lco_addr = (uint32_t)(uintptr_t)lco;
+    // Plane chunks alternate between two LDS buffers, so one barrier per chunk
+    // suffices: a wave staging chunk c+1 has passed barrier c, which every wave
+    // reached only after it finished reading chunk c-1 from that buffer.
+    int buf = 0;
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
         const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
@@ -213,15 +218,16 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
             for (int j0 = 0; j0 < a.nin; j0 += JC) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
-                stage_inputs<NW, PER, true>(a, seg, c, lds, lane, wave, j0, jn, pass == 0);
-                __syncthreads();
+                stage_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0);
+                lds_barrier();
                 if (cnt > 0) {
 #pragma nounroll
                     for (int jj = 0; jj < jn; jj++)
-                        jt_input(acc, lds_addr + (uint32_t)(jj * 8 * 64 * 4),
-                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2));
+                        jt_input(acc, lds_addr + (uint32_t)((buf * JC + jj) * 8 * 64 * 4),
+                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2),
+                                 (uint32_t)(OPW - cnt));
                 }
-                __syncthreads();
+                buf ^= 1;
             }
             uint32_t rows[OPW][8];
 #pragma unroll
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 template <int NW>
 size_t jt_lds_bytes(const RsArgs &a) {
     const int npass = a.nout > 0 ? (a.nout + NW * kJtRows - 1) / (NW * kJtRows) : 1;
-    return (size_t)2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
+    return (size_t)2 * 2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
 }
 
 
@@ -258,19 +264,11 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<std::vector<int>> sets;
-    {
-        std::vector<int> s;
-        for (int i = 51; i < 80; i++) s.push_back(i);
-        sets.push_back(s);
-    }
-    {
-        std::mt19937 rng(29);
-        std::vector<int> all(n);
-        for (int i = 0; i < n; i++) all[i] = i;
-        std::shuffle(all.begin(), all.end(), rng);
-        std::vector<int> s(all.begin(), all.begin() + k);
-        std::sort(s.begin(), s.end());
-        sets.push_back(s);
+    for (int m : {29, 22, 20, 18, 16}) {
+        std::vector<int> st;
+        for (int i = 0; i < k - m; i++) st.push_back(i);
+        for (int i = 0; i < m; i++) st.push_back(51 + i);
+        sets.push_back(st);
     }
     int set_idx = -1;
     for (auto &ids : sets) {
@@ -359,11 +357,10 @@ int main(int argc, char **argv) {
                    ok ? "ok" : "WRONG");
             fflush(stdout);
         };
-        const size_t sh2 = dma_lds_bytes<4, 2>(a), sh4 = dma_lds_bytes<4, 4>(a), sh3 = dma_lds_bytes<4, 3>(a);
         for (int rep = 0; rep < 2; rep++) {
-            timeit("dma NW4 JC8 grid4x", sh2, [&](size_t sh) { hipLaunchKernelGGL((dec_dma<4, 2>), dim3(cus * 4), dim3(256), sh, 0, a); });
-            timeit("product jt NW4 grid4x", jt_lds_bytes<4>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(cus * 4), dim3(256), sh, 0, a); });
-            if (R <= 16) timeit("product jt NW2 grid8x", jt_lds_bytes<2>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(cus * 8), dim3(128), sh, 0, a); });
+            timeit("jt NW2 grid8x", jt_lds_bytes<2>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(cus * 8), dim3(128), sh, 0, a); });
+            timeit("jt NW3 grid5x", jt_lds_bytes<3>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<3>), dim3(cus * 5), dim3(192), sh, 0, a); });
+            timeit("jt NW4 grid4x", jt_lds_bytes<4>(a), [&](size_t sh) { hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(cus * 4), dim3(256), sh, 0, a); });
         }
     }
     return 0;
