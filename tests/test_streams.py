@@ -360,3 +360,19 @@ def test_read_stripes_unexpected_next_stripe(make_rs):
     data, count = sr.read_stripes(0)
     assert count >= 1 and len(data) == count * 2048
     sr.close()
+
+
+def test_error_detection_runs(make_rs):
+    """forceErrorDetection over long runs (§8f row 3): RS(29,80), 64
+    stripes, 36 pieces offered of which 3 return random bytes; every run of
+    stripes is corrected by one Decode (Berlekamp-Welch, e = 3)."""
+    k, n, ess, stripes = 29, 80, 256, 64
+    rs = make_rs(k, n, ess)
+    data = os.urandom(stripes * k * ess)
+    pieces = _read_all_pieces(streams.encode_reader2(io.BytesIO(data), rs))
+    nums = sorted(np.random.default_rng(11).choice(n, 36, replace=False).tolist())
+    bad = set(nums[::12])  # 3 corrupted pieces
+    rmap = {i: _byte_reader(os.urandom(len(pieces[i])) if i in bad else pieces[i]) for i in nums}
+    dec = streams.decode_readers2(rmap, rs, len(data), 0, True, out_buffer=len(data))
+    assert streams.read_all(dec) == data
+    dec.close()

@@ -21,8 +21,11 @@ What differs from the reference is only where the arithmetic happens:
   * decode: ReadStripes' per-stripe Rebuild (stripe.go:407-413) becomes one
     batched rebuild of every stripe found ready (scheme.rebuild_stripes ->
     ec_rebuild_segments_host: one share choice and one inversion per ready
-    set).  With error detection each stripe still goes through Decode
-    (Berlekamp-Welch), as the reference does.
+    set).  With error detection the run goes through one Decode (Correct +
+    Rebuild, Berlekamp-Welch on the flagged byte columns) instead of one per
+    stripe: a column that cannot be corrected fails the run, and ReadStripes
+    then asks for one more share and starts over, as the reference does for
+    a failing stripe (stripe.go:419-424).
 
 A reader here is any object with read(n) -> bytes (b"" at end of stream,
 an exception on error) and close().  The scheme is an RSScheme (GPU); tests
@@ -458,11 +461,13 @@ class StripeReader:
         if not self.error_detection:
             views = [p.buf[lo * ess:hi * ess] for p in ready]
             return self.scheme.rebuild_stripes([p.num for p in ready], views, hi - lo).tobytes()
-        out = bytearray()
-        for s in range(lo, hi):
-            shares = [Share(p.num, p.buf[s * ess:(s + 1) * ess].copy()) for p in ready]
-            out += self.scheme.decode(None, shares).tobytes()
-        return bytes(out)
+        # Reed-Solomon is column-independent, so the run's bytes of each piece
+        # form one long share: a single Decode (Correct + Rebuild) covers every
+        # stripe of the run; its [k][run*ess] output is re-laid stripe-major.
+        k, m = self.scheme.required_count(), hi - lo
+        shares = [Share(p.num, p.buf[lo * ess:hi * ess].copy()) for p in ready]
+        out = self.scheme.decode(None, shares)
+        return np.ascontiguousarray(out[:k * m * ess].reshape(k, m, ess).transpose(1, 0, 2)).tobytes()
 
     def close(self):
         """Close (stripe.go:230-240): release the piece threads; does not
