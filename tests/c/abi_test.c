@@ -1,0 +1,154 @@
+/* C-ABI test from plain C -- the view a cgo binding has of the engine
+ * (INTEGRATION.md §2): include/uplink_ec.h + libuplink_ec.so, host buffers,
+ * no Python or torch in the process.  Checks every ErasureScheme export and
+ * the host-memory batch pipeline against the CPU oracle (test
+ * infrastructure: oracle/infectious_oracle.c), plus the pinned error codes
+ * and strings.  Built by `make -C tests/c`, run by tests/test_c_abi.py on a
+ * GPU box.  Exit status 0 = all checks passed. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "uplink_ec.h"
+
+/* oracle (CPU restatement of storj.io/infectious) */
+int or_new_fec(int k, int n, uint8_t *enc_matrix, uint8_t *vand_matrix);
+int or_encode(int k, int n, const uint8_t *enc, const uint8_t *in, size_t in_len, uint8_t *out);
+int or_decode(int k, int n, const uint8_t *enc, int ns, int *numbers, uint8_t **data, size_t len, uint8_t *out);
+int or_baseline_encode_segment(int k, int n, int ess, const uint8_t *enc, const uint8_t *seg, size_t stripes,
+                               uint8_t *pieces, int threads);
+
+static int failures = 0;
+#define CHECK(cond, ...)                                                                                \
+    do {                                                                                                \
+        if (!(cond)) {                                                                                  \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);                                        \
+            fprintf(stderr, __VA_ARGS__);                                                               \
+            fprintf(stderr, "\n");                                                                      \
+            failures++;                                                                                 \
+        }                                                                                               \
+    } while (0)
+
+static uint64_t rng_state = 0x5EED0000ull;
+static uint8_t rnd8(void) {
+    rng_state = rng_state * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint8_t)(rng_state >> 56);
+}
+static void fill(uint8_t *p, size_t n) {
+    for (size_t i = 0; i < n; i++) p[i] = rnd8();
+}
+
+static void scheme_surface(int k, int n, int ess) {
+    ec_ctx *ctx = NULL;
+    int rc = ec_create(k, n, ess, &ctx);
+    CHECK(rc == EC_OK, "ec_create(%d,%d,%d) = %d (%s)", k, n, ess, rc, ec_strerror(rc));
+    if (rc) return;
+    CHECK(ec_required(ctx) == k && ec_total(ctx) == n && ec_share_size(ctx) == ess &&
+              ec_stripe_size(ctx) == k * ess,
+          "sizes");
+    uint8_t *enc = malloc((size_t)n * k), *vand = malloc((size_t)n * k);
+    or_new_fec(k, n, enc, vand);
+    uint8_t *g = malloc((size_t)n * k);
+    ec_generator(ctx, g);
+    CHECK(memcmp(g, enc, (size_t)n * k) == 0, "generator != oracle enc_matrix (%d,%d)", k, n);
+
+    const size_t stripe = (size_t)k * ess;
+    uint8_t *in = malloc(stripe), *all = malloc((size_t)n * ess), *ref = malloc((size_t)n * ess);
+    uint8_t *one = malloc(ess);
+    fill(in, stripe);
+    CHECK(ec_encode(ctx, in, stripe, all) == EC_OK, "ec_encode");
+    or_encode(k, n, enc, in, stripe, ref);
+    CHECK(memcmp(all, ref, (size_t)n * ess) == 0, "ec_encode != oracle (%d,%d,%d)", k, n, ess);
+    for (int num = 0; num < n; num += (n > 8 ? n / 8 : 1)) {
+        CHECK(ec_encode_single(ctx, in, stripe, one, ess, num) == EC_OK, "ec_encode_single");
+        CHECK(memcmp(one, ref + (size_t)num * ess, ess) == 0, "ec_encode_single num=%d", num);
+    }
+    /* pinned error strings (segmentupload/encode_test.go:53,63) */
+    char msg[128];
+    rc = ec_encode_single(ctx, in, stripe, one, ess, -1);
+    CHECK(rc == EC_ERR_NUM_NEGATIVE, "num -1 -> %d", rc);
+    ec_format_error(ctx, rc, 0, msg, sizeof msg);
+    CHECK(strcmp(msg, "num must be non-negative") == 0, "msg '%s'", msg);
+    rc = ec_encode_single(ctx, in, stripe, one, ess, n);
+    CHECK(rc == EC_ERR_NUM_RANGE, "num n -> %d", rc);
+    ec_format_error(ctx, rc, 0, msg, sizeof msg);
+    char want[64];
+    snprintf(want, sizeof want, "num must be less than %d", n);
+    CHECK(strcmp(msg, want) == 0, "msg '%s' want '%s'", msg, want);
+
+    /* Rebuild / Decode from the last k shares (all parity when n >= 2k) */
+    int nums[256];
+    const uint8_t *shp[256];
+    uint8_t *shw[256];
+    uint8_t *out = malloc(stripe), *out2 = malloc(stripe);
+    for (int i = 0; i < k; i++) {
+        nums[i] = n - k + i;
+        shp[i] = all + (size_t)(n - k + i) * ess;
+    }
+    CHECK(ec_rebuild(ctx, k, nums, shp, ess, out) == EC_OK, "ec_rebuild");
+    CHECK(memcmp(out, in, stripe) == 0, "ec_rebuild != input (%d,%d,%d)", k, n, ess);
+    if (n - k >= 2) {
+        /* Decode with 2 extra shares, one of them corrupted: Berlekamp-Welch */
+        int ns = k + 2;
+        for (int i = 0; i < ns; i++) {
+            nums[i] = n - ns + i;
+            shw[i] = malloc(ess);
+            memcpy(shw[i], all + (size_t)(n - ns + i) * ess, ess);
+        }
+        shw[1][ess / 2] ^= 0x5a;
+        uint8_t *cp[256];
+        int cn[256];
+        for (int i = 0; i < ns; i++) {
+            cp[i] = malloc(ess);
+            memcpy(cp[i], shw[i], ess);
+            cn[i] = nums[i];
+        }
+        rc = ec_decode(ctx, ns, nums, shw, ess, out);
+        CHECK(rc == EC_OK, "ec_decode rc %d", rc);
+        CHECK(memcmp(out, in, stripe) == 0, "ec_decode did not correct (%d,%d)", k, n);
+        rc = or_decode(k, n, enc, ns, cn, cp, ess, out2);
+        CHECK(rc == 0 && memcmp(out2, in, stripe) == 0, "oracle decode");
+        for (int i = 0; i < ns; i++) {
+            free(shw[i]);
+            free(cp[i]);
+        }
+    }
+    /* NotEnoughShares */
+    rc = ec_rebuild(ctx, k - 1, nums, shp, ess, out);
+    CHECK(rc == EC_ERR_NOT_ENOUGH_SHARES, "k-1 shares -> %d", rc);
+
+    /* host-memory batch pipeline: 3 segments of 5 stripes */
+    const size_t nseg = 3, stripes = 5, spad = stripes * stripe, plen = stripes * (size_t)ess;
+    uint8_t *segs = malloc(nseg * spad), *pieces = malloc(nseg * (size_t)n * plen), *pref = malloc((size_t)n * plen);
+    uint8_t *back = malloc(nseg * spad);
+    fill(segs, nseg * spad);
+    CHECK(ec_encode_segments_host(ctx, segs, nseg, stripes, pieces, 0) == EC_OK, "ec_encode_segments_host");
+    for (size_t s = 0; s < nseg; s++) {
+        or_baseline_encode_segment(k, n, ess, enc, segs + s * spad, stripes, pref, 1);
+        CHECK(memcmp(pieces + s * (size_t)n * plen, pref, (size_t)n * plen) == 0, "segment %zu pieces", s);
+    }
+    const uint8_t *pp[256];
+    for (int i = 0; i < k; i++) {
+        nums[i] = n - 1 - i; /* any order */
+        pp[i] = pieces + (size_t)(n - 1 - i) * plen;
+    }
+    CHECK(ec_rebuild_segments_host(ctx, k, nums, pp, stripes, nseg, (long long)n * plen, back) == EC_OK,
+          "ec_rebuild_segments_host");
+    CHECK(memcmp(back, segs, nseg * spad) == 0, "rebuilt segments != input (%d,%d,%d)", k, n, ess);
+
+    free(segs), free(pieces), free(pref), free(back);
+    free(in), free(all), free(ref), free(one), free(out), free(out2), free(enc), free(vand), free(g);
+    ec_destroy(ctx);
+}
+
+int main(void) {
+    ec_ctx *bad = NULL;
+    CHECK(ec_create(0, 4, 256, &bad) == EC_ERR_PARAMS, "k = 0");
+    CHECK(ec_create(5, 4, 256, &bad) == EC_ERR_PARAMS, "k > n");
+    CHECK(ec_device_count() >= 1, "no device");
+    const int cfg[][3] = {{2, 4, 1024}, {4, 10, 256}, {29, 80, 256}, {20, 60, 4096}, {3, 7, 100}, {10, 20, 64}};
+    for (size_t i = 0; i < sizeof cfg / sizeof cfg[0]; i++) scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2]);
+    printf("%s: %d failures\n", failures ? "FAIL" : "ok", failures);
+    return failures ? 1 : 0;
+}
