@@ -418,3 +418,22 @@ def test_c1_loopback_piecestore(oracle):
     for nums in ([6, 7, 8, 9], sorted(rng.choice(n, k, replace=False).tolist())):
         out = gpu_rebuild(rs.scheme, d_pieces, nums, stripes)[0]
         assert eestream.unpad(out.tobytes()) == data
+
+
+def test_unsafe_rs_scheme_decode_is_rebuild(oracle):
+    """NewUnsafeRSScheme (unsafe_rs.go:32-52): Decode = Rebuild into out,
+    no correction -- a corrupted share among the chosen k shows through,
+    where RSScheme.Decode corrects it."""
+    k, n, ess = 4, 10, 512
+    fc = eestream.new_fec(k, n)
+    safe, unsafe = eestream.RSScheme(fc, ess), eestream.new_unsafe_rs_scheme(fc, ess)
+    stripe = np.random.default_rng(21).integers(0, 256, k * ess, dtype=np.uint8)
+    allsh = oracle.FEC(k, n).encode(stripe)
+    shares = [eestream.Share(i, np.array(allsh[i])) for i in (9, 7, 5, 3)]
+    out = np.zeros(k * ess + 7, dtype=np.uint8)
+    got = unsafe.decode(out, shares)
+    assert np.array_equal(got, stripe) and got.base is out or np.shares_memory(got, out)
+    bad = [eestream.Share(i, np.array(allsh[i])) for i in (0, 2, 4, 6, 8, 9)]
+    bad[1].data[3] ^= 0x41  # share 2: one of the shares Rebuild takes
+    assert not np.array_equal(unsafe.decode(None, [s.deep_copy() for s in bad]), stripe)
+    assert np.array_equal(safe.decode(None, bad), stripe)

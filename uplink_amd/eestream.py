@@ -7,6 +7,7 @@ parity tests read like the reference's own tests:
   new_fec / FEC                  eestream.NewFEC               private/eestream/fec.go:15-17
   Share                          infectious.Share              private/eestream/fec.go:9
   RSScheme (ErasureScheme)       rsScheme                      private/eestream/rs.go:11-61
+  UnsafeRSScheme                 unsafeRSScheme (no Correct)   private/eestream/unsafe_rs.go:11-73
     .encode / .encode_single / .decode / .rebuild / sizes     scheme.go:13-41
   RedundancyStrategy             encode.go:23-99 (threshold validation + errors)
   calc_piece_size                CalcPieceSize                 encode.go:272-281
@@ -264,6 +265,26 @@ class RSScheme:
 
 def new_rs_scheme(fc: FEC, erasure_share_size: int) -> RSScheme:
     return RSScheme(fc, erasure_share_size)
+
+
+class UnsafeRSScheme(RSScheme):
+    """unsafeRSScheme (unsafe_rs.go:11-73): Decode is Rebuild into out (the k
+    data shares at number * ess), without error correction."""
+
+    def decode(self, out: Optional[np.ndarray], shares: List[Share]) -> np.ndarray:
+        ln = len(shares[0].data) if shares else 0
+        need = self.fc.k * ln
+        dst = out[:need] if (out is not None and out.size >= need) else np.zeros(max(need, 1), dtype=np.uint8)[:need]
+
+        def put(sh: Share):
+            dst[sh.number * ln:(sh.number + 1) * ln] = sh.data
+        self.rebuild(shares, put)
+        return dst
+
+
+def new_unsafe_rs_scheme(fc: FEC, erasure_share_size: int) -> UnsafeRSScheme:
+    """NewUnsafeRSScheme (unsafe_rs.go:16-19)."""
+    return UnsafeRSScheme(fc, erasure_share_size)
 
 
 # ------------------------------------------------------------------ strategy
