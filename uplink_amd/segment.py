@@ -1,0 +1,212 @@
+"""Segment-level upload integration of the encoder.
+
+Mirrors, on the engine:
+
+  PinnedBackend           buffer.Backend / MemoryBackend   private/storage/streams/buffer/backend.go:12-120
+                          (the segment buffer, swappable via Splitter.NewBackend,
+                          splitter/splitter.go:87-89) -- here in pinned host memory
+                          (ec_host_alloc) so the segment crosses PCIe at full DMA rate
+  SegmentPieceReader      pieceReader.PieceReader          private/storage/streams/segmentupload/single.go:228-238
+
+The reference's PieceReader(num) re-reads the whole segment through
+PadReader and runs EncodeSingle once per stripe for each of the n pieces
+(n readers x stripes calls, and n passes over the segment).  Here the first
+request pads the segment once and encodes every parity piece of every
+stripe in one engine call (ec_encode_segments_host with
+EC_FLAG_PARITY_ONLY); data pieces (num < k) are the segment's own shares
+(EncodeSingle copies them, rs.go:21-23) and are served from the padded
+segment, so only the n - k parity pieces come back over PCIe.
+"""
+from __future__ import annotations
+
+import ctypes
+import io
+import threading
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+from .eestream import EEStreamError, InfectiousError, _raise
+
+STANDARD_MAX_ENCRYPTED_SEGMENT_SIZE = 67254016  # buffer/backend.go:20
+
+
+class PinnedHost:
+    """A pinned host allocation (hipHostMalloc via ec_host_alloc) viewed as
+    a numpy uint8 array; freed by close()."""
+
+    def __init__(self, nbytes: int):
+        self._lib = N.load()
+        self.nbytes = max(int(nbytes), 1)
+        self.ptr = self._lib.ec_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"ec_host_alloc({self.nbytes}) failed")
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self._lib.ec_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _Pool:
+    """Pinned allocations are slow to make (hipHostMalloc pins pages); keep
+    freed ones for reuse by size (the role of sync.Pool in backend.go:25-38)."""
+
+    def __init__(self):
+        self._mu = threading.Lock()
+        self._free = {}
+
+    def get(self, nbytes: int) -> PinnedHost:
+        with self._mu:
+            lst = self._free.get(max(int(nbytes), 1))
+            if lst:
+                return lst.pop()
+        return PinnedHost(nbytes)
+
+    def put(self, buf: PinnedHost):
+        if buf.ptr:
+            with self._mu:
+                self._free.setdefault(buf.nbytes, []).append(buf)
+
+
+pinned_pool = _Pool()
+
+
+class PinnedBackend:
+    """buffer.Backend (io.Writer + io.ReaderAt + io.Closer) on pinned host
+    memory, like NewMemoryBackend(cap) (backend.go:42-52)."""
+
+    def __init__(self, cap: int = STANDARD_MAX_ENCRYPTED_SEGMENT_SIZE):
+        self._mem = pinned_pool.get(cap)
+        self._cap = cap
+        self._size = 0
+        self._mu = threading.Lock()
+        self._closed = False
+
+    def write(self, b) -> int:
+        with self._mu:
+            if self._closed:
+                raise EEStreamError("write to closed backend")
+            b = memoryview(b).cast("B")
+            n = len(b)
+            if self._size + n > self._cap:
+                raise io.UnsupportedOperation("write past the backend capacity")  # MemoryBackend: io.ErrShortWrite
+            self._mem.array[self._size:self._size + n] = np.frombuffer(b, dtype=np.uint8)
+            self._size += n
+            return n
+
+    def read_at(self, n: int, off: int) -> bytes:
+        with self._mu:
+            if self._closed:
+                raise EEStreamError("read from closed backend")
+            if off >= self._size:
+                return b""
+            return self._mem.array[off:min(off + n, self._size)].tobytes()
+
+    def size(self) -> int:
+        return self._size
+
+    def view(self) -> np.ndarray:
+        """The written bytes, zero-copy."""
+        return self._mem.array[:self._size]
+
+    def close(self):
+        with self._mu:
+            if not self._closed:
+                self._closed = True
+                pinned_pool.put(self._mem)
+                self._mem = None
+        return None
+
+    def _scratch_tail(self, total: int) -> Optional[PinnedHost]:
+        """The backing allocation when it can also hold `total` bytes (the
+        written data plus PadReader's padding), else None."""
+        return self._mem if (not self._closed and self._mem.nbytes >= total) else None
+
+
+class _PieceStream:
+    def __init__(self, src: np.ndarray):
+        self._src, self._off = src, 0
+
+    def read(self, n: int = -1) -> bytes:
+        end = self._src.size if n is None or n < 0 else min(self._src.size, self._off + n)
+        b = self._src[self._off:end].tobytes()
+        self._off = end
+        return b
+
+    def close(self):
+        return None
+
+
+class SegmentPieceReader:
+    """pieceReader (single.go:228-238): piece_reader(num) streams piece num
+    of the segment (PadReader to the stripe size, then EncodeSingle per
+    stripe).  The first call pads and encodes the whole segment once."""
+
+    def __init__(self, segment, redundancy):
+        self.segment = segment  # bytes-like, numpy array, or PinnedBackend
+        self.redundancy = redundancy
+        self._mu = threading.Lock()
+        self._padded: Optional[np.ndarray] = None
+        self._parity: Optional[PinnedHost] = None
+        self._bufs = []
+        self.stripes = 0
+
+    def _prepare(self):
+        with self._mu:
+            if self._padded is not None:
+                return
+            rs = self.redundancy
+            k, n, ess = rs.required_count(), rs.total_count(), rs.erasure_share_size()
+            stripe = rs.stripe_size()
+            data = self.segment.view() if isinstance(self.segment, PinnedBackend) else np.frombuffer(
+                memoryview(self.segment).cast("B"), dtype=np.uint8)
+            size = data.size
+            # PadReader: p = 4 + (stripe - (size+4) % stripe) % stripe bytes
+            p = 4 + (stripe - (size + 4) % stripe) % stripe
+            stripes = (size + p) // stripe
+            own = self.segment._scratch_tail(size + p) if isinstance(self.segment, PinnedBackend) else None
+            if own is not None:  # pad in place, right after the segment in its own pinned buffer
+                padded = own
+            else:
+                padded = pinned_pool.get(stripes * stripe)
+                padded.array[:size] = data
+                self._bufs.append(padded)
+            padded.array[size:size + p] = p & 0xFF
+            padded.array[size + p - 4:size + p] = np.frombuffer(p.to_bytes(4, "big"), dtype=np.uint8)
+            parity = pinned_pool.get((n - k) * stripes * ess)
+            self._bufs.append(parity)
+            if n > k:
+                rc = N.load().ec_encode_segments_host(rs.scheme.ctx if hasattr(rs, "scheme") else rs.ctx, padded.ptr,
+                                                      1, stripes, parity.ptr, N.EC_FLAG_PARITY_ONLY)
+                _raise(None, rc)
+            self.stripes = stripes
+            self._padded = padded.array[:stripes * stripe].reshape(stripes, k, ess)
+            self._parity = parity.array[:(n - k) * stripes * ess].reshape(n - k, stripes * ess)
+
+    def piece_reader(self, num: int):
+        rs = self.redundancy
+        k, n = rs.required_count(), rs.total_count()
+        if num < 0:  # infectious EncodeSingle's errors (segmentupload/encode_test.go:53,63)
+            raise InfectiousError("num must be non-negative")
+        if num >= n:
+            raise InfectiousError(f"num must be less than {n}")
+        self._prepare()
+        if num < k:  # EncodeSingle of a data share is the share itself (rs.go:21-23)
+            return _PieceStream(np.ascontiguousarray(self._padded[:, num, :]).reshape(-1))
+        return _PieceStream(self._parity[num - k])
+
+    def close(self):
+        for b in self._bufs:
+            pinned_pool.put(b)
+        self._bufs = []
+        self._padded = self._parity = None
