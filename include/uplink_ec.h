@@ -26,6 +26,9 @@
  *   ec_rebuild_segments      batch form of the per-stripe Rebuild loop of
  *                            StripeReader.ReadStripes  stripe.go:382-428
  *   ec_*_segments_host       the same batches from/to host memory (PCIe pipeline)
+ *   ec_*blake3* / ec_hash_segments / ec_encode_segments_host_hashed
+ *                            BLAKE3 piece hash of the upload (piecestore/upload.go:
+ *                            133,155,270; hash.go:20-26), SURVEY §8f row 4
  *   ec_strerror/ec_format_error  error texts of infectious / eestream
  *
  * Error codes map to the errors eestream's callers test:
@@ -134,8 +137,34 @@ int ec_encode_segments_host(const ec_ctx *ctx, const uint8_t *segs, size_t nseg,
  * that share is at pieces[i] + g*piece_seg_stride. out: [nseg][stripes*k*ess] */
 int ec_rebuild_segments_host(const ec_ctx *ctx, int nshares, const int *nums, const uint8_t *const *pieces,
                              size_t nstripes, size_t nseg, long long piece_seg_stride, uint8_t *out);
+/* ec_encode_segments_host + the BLAKE3-256 hash of every piece (all n, also
+ * with EC_FLAG_PARITY_ONLY): hashes = [nseg][n][32] host bytes, the value
+ * piecestore's upload sends as PieceHash.Hash (piecestore/upload.go:133,155,270)
+ * when the piece hash algorithm is BLAKE3 (the default, piecestore/hash.go:20-26). */
+int ec_encode_segments_host_hashed(const ec_ctx *ctx, const uint8_t *segs, size_t nseg, size_t nstripes,
+                                   uint8_t *pieces, uint8_t *hashes, int flags);
 void *ec_host_alloc(size_t bytes); /* pinned (hipHostMalloc); NULL on failure */
 void ec_host_free(void *p);
+
+/* ---- BLAKE3-256 piece hashes (github.com/zeebo/blake3 v0.2.3, go.mod:29) ----
+ * Replace the per-piece hash.Hash fed by io.TeeReader during upload
+ * (piecestore/upload.go:133 NewHashFromAlgorithm, :155 TeeReader, :270
+ * Sum(nil)); 32-byte digests, BLAKE3 hash mode, no key. */
+
+/* Device pieces: byte t of piece j is at
+ *   base + j*piece_stride + (t / run)*run_stride + t % run
+ * (run = piece_len or 0 for contiguous pieces).  hashes: npieces*32 device
+ * bytes.  Async on stream (scratch from hipMallocAsync on that stream). */
+int ec_blake3_pieces(const uint8_t *base, size_t npieces, long long piece_stride, size_t piece_len, size_t run,
+                     long long run_stride, uint8_t *hashes, ec_stream stream);
+/* Every piece of nseg segments already on the device: data piece j of
+ * segment s is share j of each stripe of segs + s*nstripes*k*ess; parity
+ * piece k+r is parity + (s*(n-k) + r)*nstripes*ess (the EC_FLAG_PARITY_ONLY
+ * output).  hashes: [nseg][n][32] device bytes.  Async on stream. */
+int ec_hash_segments(const ec_ctx *ctx, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,
+                     uint8_t *hashes, ec_stream stream);
+/* Host buffers, synchronous: hashes[32*j] = BLAKE3(data + j*stride, piece_len) */
+int ec_blake3_host(const uint8_t *data, size_t npieces, long long stride, size_t piece_len, uint8_t *hashes);
 
 /* ---- device helpers ---- */
 int ec_device_count(void);

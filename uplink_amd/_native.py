@@ -58,6 +58,12 @@ SIGNATURES = {
     "ec_encode_segments_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, ctypes.c_int]),
     "ec_rebuild_segments_host": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
                                                 ctypes.c_size_t, ctypes.c_size_t, ctypes.c_longlong, vp]),
+    "ec_encode_segments_host_hashed": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, vp,
+                                                      ctypes.c_int]),
+    "ec_blake3_pieces": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_size_t,
+                                        ctypes.c_longlong, vp, vp]),
+    "ec_hash_segments": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, vp]),
+    "ec_blake3_host": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_size_t, vp]),
     "ec_host_alloc": (vp, [ctypes.c_size_t]),
     "ec_host_free": (None, [vp]),
     "ec_device_count": (ctypes.c_int, []),

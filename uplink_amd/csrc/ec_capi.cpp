@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/uplink_ec.h"
+#include "blake3.hpp"
 #include "gf256.hpp"
 #include "rs_correct.hpp"
 #include "rs_kernels.hpp"
@@ -599,30 +600,135 @@ void ec_host_free(void *p) {
 // kernel, then D2H, all stream-ordered, so a slot's device buffers are never
 // reused before its previous segment has left the GPU; the three streams
 // overlap the copies of neighbouring segments with each other and the kernel.
-int ec_encode_segments_host(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
-                            int flags) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// BLAKE3 of every piece of one segment resident on the device: parity pieces
+// are contiguous in `parity` ([n-k][plen]), data piece j is share j of every
+// stripe of the stripe-major segment `seg` (runs of ess bytes, k*ess apart).
+// hashes: n*32 device bytes; ws: b3_segment_ws_bytes.
+static B3View data_view(const ec_ctx *c, const uint8_t *seg, size_t nstripes) {
+    return B3View{seg, (int64_t)c->ess, nstripes * (uint64_t)c->ess, (uint64_t)c->ess, (int64_t)c->k * c->ess,
+                  (uint64_t)c->k, 0};
+}
+static B3View parity_view(const ec_ctx *c, const uint8_t *parity, size_t nstripes) {
+    const uint64_t plen = nstripes * (uint64_t)c->ess;
+    return B3View{parity, (int64_t)plen, plen, plen, (int64_t)plen, (uint64_t)(c->n - c->k), 0};
+}
+static size_t b3_segment_ws_bytes(const ec_ctx *c, size_t nstripes) {
+    return align_up(std::max(b3_workspace_bytes(data_view(c, nullptr, nstripes)),
+                             b3_workspace_bytes(parity_view(c, nullptr, nstripes))),
+                    256);
+}
+static int hash_segment(const ec_ctx *c, const uint8_t *seg, const uint8_t *parity, size_t nstripes, uint8_t *hashes,
+                        uint8_t *ws, hipStream_t st) {
+    HIP_TRY(b3_launch(data_view(c, seg, nstripes), hashes, ws, st));
+    if (c->n > c->k) HIP_TRY(b3_launch(parity_view(c, parity, nstripes), hashes + 32 * (size_t)c->k, ws, st));
+    return EC_OK;
+}
+
+static int encode_host(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                       uint8_t *hashes, int flags) {
     if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
     if (nseg == 0 || nstripes == 0) return EC_OK;
     const size_t spad = nstripes * (size_t)c->k * c->ess;
-    const int rows = (flags & EC_FLAG_PARITY_ONLY) ? c->n - c->k : c->n;
+    const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
+    const int rows = parity_only ? c->n - c->k : c->n;
     const size_t pbytes = (size_t)rows * nstripes * c->ess;
+    // device slot: pieces | hashes (n*32) | BLAKE3 workspace
+    const size_t hash_at = align_up(pbytes, 256), ws_at = hash_at + align_up(32 * (size_t)c->n, 256);
+    const size_t out_cap = hashes ? ws_at + b3_segment_ws_bytes(c, nstripes) : pbytes;
     std::lock_guard<std::mutex> g(c->pipe_mu);
-    int rc = pipe_reserve(c, spad, pbytes);
+    int rc = pipe_reserve(c, spad, out_cap);
     if (rc) return rc;
     for (size_t s = 0; s < nseg && rc == EC_OK; s++) {
         const int slot = (int)(s % HostPipe::kSlots);
         hipStream_t st = c->pipe.st[slot];
+        uint8_t *d_out = c->pipe.d_out[slot];
         if (hipMemcpyAsync(c->pipe.d_in[slot], segs + s * spad, spad, hipMemcpyHostToDevice, st) != hipSuccess) {
             rc = EC_ERR_DEVICE;
             break;
         }
-        rc = ec_encode_segments(c, c->pipe.d_in[slot], 1, nstripes, c->pipe.d_out[slot], flags, st);
+        if (rows > 0) rc = ec_encode_segments(c, c->pipe.d_in[slot], 1, nstripes, d_out, flags, st);
         if (rc) break;
-        if (hipMemcpyAsync(pieces + s * pbytes, c->pipe.d_out[slot], pbytes, hipMemcpyDeviceToHost, st) != hipSuccess)
+        if (hashes) {
+            const uint8_t *parity = d_out + (parity_only ? 0 : (size_t)c->k * nstripes * c->ess);
+            rc = hash_segment(c, c->pipe.d_in[slot], parity, nstripes, d_out + hash_at, d_out + ws_at, st);
+            if (rc) break;
+            if (hipMemcpyAsync(hashes + s * 32 * (size_t)c->n, d_out + hash_at, 32 * (size_t)c->n,
+                               hipMemcpyDeviceToHost, st) != hipSuccess) {
+                rc = EC_ERR_DEVICE;
+                break;
+            }
+        }
+        if (pbytes && hipMemcpyAsync(pieces + s * pbytes, d_out, pbytes, hipMemcpyDeviceToHost, st) != hipSuccess)
             rc = EC_ERR_DEVICE;
     }
     return pipe_drain(c, rc);
+}
+
+int ec_encode_segments_host(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                            int flags) {
+    return encode_host(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, pieces, nullptr, flags);
+}
+
+int ec_encode_segments_host_hashed(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes,
+                                   uint8_t *pieces, uint8_t *hashes, int flags) {
+    if (!hashes) return EC_ERR_INVALID_ARG;
+    return encode_host(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, pieces, hashes, flags);
+}
+
+int ec_hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,
+                     uint8_t *hashes, ec_stream stream) {
+    if (!c || !segs || !hashes || (c->n > c->k && !parity)) return EC_ERR_INVALID_ARG;
+    if (nseg == 0) return EC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t ws_bytes = b3_segment_ws_bytes(c, nstripes);
+    void *ws = nullptr;
+    if (ws_bytes) HIP_TRY(hipMallocAsync(&ws, ws_bytes, st));
+    int rc = EC_OK;
+    const size_t spad = nstripes * (size_t)c->k * c->ess, pbytes = (size_t)(c->n - c->k) * nstripes * c->ess;
+    for (size_t s = 0; s < nseg && rc == EC_OK; s++)
+        rc = hash_segment(c, segs + s * spad, parity ? parity + s * pbytes : nullptr, nstripes,
+                          hashes + s * 32 * (size_t)c->n, (uint8_t *)ws, st);
+    if (ws) (void)hipFreeAsync(ws, st);
+    return rc;
+}
+
+int ec_blake3_pieces(const uint8_t *base, size_t npieces, long long piece_stride, size_t piece_len, size_t run,
+                     long long run_stride, uint8_t *hashes, ec_stream stream) {
+    if (!hashes || (!base && piece_len && npieces)) return EC_ERR_INVALID_ARG;
+    if (npieces == 0) return EC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const B3View v{base, piece_stride, piece_len, run, run_stride, npieces, 0};
+    const size_t ws_bytes = b3_workspace_bytes(v);
+    void *ws = nullptr;
+    if (ws_bytes) HIP_TRY(hipMallocAsync(&ws, ws_bytes, st));
+    const hipError_t e = b3_launch(v, hashes, ws, st);
+    if (ws) (void)hipFreeAsync(ws, st);
+    return hip_fail(e);
+}
+
+int ec_blake3_host(const uint8_t *data, size_t npieces, long long stride, size_t piece_len, uint8_t *hashes) {
+    if (!hashes || (!data && piece_len && npieces)) return EC_ERR_INVALID_ARG;
+    if (npieces == 0) return EC_OK;
+    const size_t span = (npieces - 1) * (size_t)stride + piece_len;
+    hipStream_t st = nullptr;
+    uint8_t *d = nullptr;
+    int rc = EC_OK;
+    do {
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipMalloc(&d, align_up(span, 256) + 32 * npieces) != hipSuccess) { rc = EC_ERR_DEVICE; d = nullptr; break; }
+        uint8_t *dh = d + align_up(span, 256);
+        if (span && hipMemcpyAsync(d, data, span, hipMemcpyHostToDevice, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        rc = ec_blake3_pieces(d, npieces, stride, piece_len, piece_len, stride, dh, st);
+        if (rc) break;
+        if (hipMemcpyAsync(hashes, dh, 32 * npieces, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipStreamSynchronize(st) != hipSuccess) rc = EC_ERR_DEVICE;
+    } while (0);
+    if (st) (void)hipStreamSynchronize(st);
+    if (d) (void)hipFree(d);
+    if (st) (void)hipStreamDestroy(st);
+    return rc;
 }
 
 int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, const uint8_t *const *pieces,

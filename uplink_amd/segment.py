@@ -152,12 +152,14 @@ class SegmentPieceReader:
     of the segment (PadReader to the stripe size, then EncodeSingle per
     stripe).  The first call pads and encodes the whole segment once."""
 
-    def __init__(self, segment, redundancy):
+    def __init__(self, segment, redundancy, hash_pieces: bool = False):
         self.segment = segment  # bytes-like, numpy array, or PinnedBackend
         self.redundancy = redundancy
+        self.hash_pieces = hash_pieces  # also compute every piece's BLAKE3 in the same engine call
         self._mu = threading.Lock()
         self._padded: Optional[np.ndarray] = None
         self._parity: Optional[PinnedHost] = None
+        self._hashes: Optional[np.ndarray] = None
         self._bufs = []
         self.stripes = 0
 
@@ -185,9 +187,14 @@ class SegmentPieceReader:
             padded.array[size + p - 4:size + p] = np.frombuffer(p.to_bytes(4, "big"), dtype=np.uint8)
             parity = pinned_pool.get((n - k) * stripes * ess)
             self._bufs.append(parity)
-            if n > k:
-                rc = N.load().ec_encode_segments_host(rs.scheme.ctx if hasattr(rs, "scheme") else rs.ctx, padded.ptr,
-                                                      1, stripes, parity.ptr, N.EC_FLAG_PARITY_ONLY)
+            ctx = rs.scheme.ctx if hasattr(rs, "scheme") else rs.ctx
+            if self.hash_pieces:  # parity + the BLAKE3 of all n pieces (piecestore/upload.go:155,270)
+                self._hashes = np.empty((n, 32), dtype=np.uint8)
+                rc = N.load().ec_encode_segments_host_hashed(ctx, padded.ptr, 1, stripes, parity.ptr,
+                                                             self._hashes.ctypes.data, N.EC_FLAG_PARITY_ONLY)
+                _raise(None, rc)
+            elif n > k:
+                rc = N.load().ec_encode_segments_host(ctx, padded.ptr, 1, stripes, parity.ptr, N.EC_FLAG_PARITY_ONLY)
                 _raise(None, rc)
             self.stripes = stripes
             self._padded = padded.array[:stripes * stripe].reshape(stripes, k, ess)
@@ -205,8 +212,18 @@ class SegmentPieceReader:
             return _PieceStream(np.ascontiguousarray(self._padded[:, num, :]).reshape(-1))
         return _PieceStream(self._parity[num - k])
 
+    def piece_hash(self, num: int) -> bytes:
+        """BLAKE3-256 of piece num: what the piecestore upload of that piece
+        sends as PieceHash.Hash (upload.go:270).  Needs hash_pieces=True."""
+        if not self.hash_pieces:
+            raise EEStreamError("piece hashes were not requested (hash_pieces=False)")
+        if not 0 <= num < self.redundancy.total_count():
+            raise InfectiousError(f"num must be less than {self.redundancy.total_count()}")
+        self._prepare()
+        return self._hashes[num].tobytes()
+
     def close(self):
         for b in self._bufs:
             pinned_pool.put(b)
         self._bufs = []
-        self._padded = self._parity = None
+        self._padded = self._parity = self._hashes = None
