@@ -28,173 +28,117 @@
 #include <hip/hip_runtime.h>
 
 #include "blake3.hpp"
+#include "blake3_device.hpp"
 
 namespace uplink_ec {
 namespace {
 
-constexpr uint32_t kChunkStart = 1, kChunkEnd = 2, kParent = 4, kRoot = 8;
-constexpr int kGroup = 256;  // chunks (or nodes) folded per workgroup
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+using namespace b3;
 
-__device__ constexpr uint32_t kIV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
-                                        0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
-
-// message word schedule: kSched[r][i] = index of the word used in slot i of
-// round r (the fixed permutation applied r times)
-struct Sched {
-    uint8_t s[7][16];
-    constexpr Sched() : s{} {
-        constexpr uint8_t perm[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
-        for (int i = 0; i < 16; i++) s[0][i] = (uint8_t)i;
-        for (int r = 1; r < 7; r++)
-            for (int i = 0; i < 16; i++) s[r][i] = s[r - 1][perm[i]];
-    }
-};
-constexpr Sched kSched{};
-
-__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
-
-__device__ __forceinline__ void G(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t x, uint32_t y) {
-    a = a + b + x;
-    d = rotr(d ^ a, 16);
-    c = c + d;
-    b = rotr(b ^ c, 12);
-    a = a + b + y;
-    d = rotr(d ^ a, 8);
-    c = c + d;
-    b = rotr(b ^ c, 7);
+// Start of piece j: pieces come in sets of `pieces_per_set` (one set per
+// segment), set_stride apart.
+__device__ __forceinline__ const uint8_t *piece_base(const B3View &v, uint64_t j) {
+    return v.base + (int64_t)(j / v.pieces_per_set) * v.set_stride + (int64_t)(j % v.pieces_per_set) * v.piece_stride;
 }
 
-// h <- first 8 words of compress(h, m, counter, blen, flags) (the new CV, or
-// the 32-byte hash when flags has ROOT)
-__device__ __forceinline__ void compress(uint32_t (&h)[8], const uint32_t (&m)[16], uint32_t ctr_lo, uint32_t ctr_hi,
-                                         uint32_t blen, uint32_t flags) {
-    uint32_t v[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = h[i];
-#pragma unroll
-    for (int i = 0; i < 4; i++) v[8 + i] = kIV[i];
-    v[12] = ctr_lo;
-    v[13] = ctr_hi;
-    v[14] = blen;
-    v[15] = flags;
-#pragma unroll
-    for (int r = 0; r < 7; r++) {
-        const uint8_t *s = kSched.s[r];
-        G(v[0], v[4], v[8], v[12], m[s[0]], m[s[1]]);
-        G(v[1], v[5], v[9], v[13], m[s[2]], m[s[3]]);
-        G(v[2], v[6], v[10], v[14], m[s[4]], m[s[5]]);
-        G(v[3], v[7], v[11], v[15], m[s[6]], m[s[7]]);
-        G(v[0], v[5], v[10], v[15], m[s[8]], m[s[9]]);
-        G(v[1], v[6], v[11], v[12], m[s[10]], m[s[11]]);
-        G(v[2], v[7], v[8], v[13], m[s[12]], m[s[13]]);
-        G(v[3], v[4], v[9], v[14], m[s[14]], m[s[15]]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) h[i] = v[i] ^ v[i + 8];
-}
-
-__device__ __forceinline__ void parent(uint32_t (&h)[8], const uint32_t (&l)[8], const uint32_t (&r)[8], bool root) {
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        m[i] = l[i];
-        m[8 + i] = r[i];
-        h[i] = kIV[i];
-    }
-    compress(h, m, 0, 0, 64, kParent | (root ? kRoot : 0));
-}
-
-// byte address of byte t of piece j
+// byte t of a piece starting at pb
 template <bool kFast>
-__device__ __forceinline__ const uint8_t *at(const B3View &v, uint64_t j, uint64_t t) {
+__device__ __forceinline__ const uint8_t *at(const B3View &v, const uint8_t *pb, uint64_t t) {
     if (kFast)  // power-of-two runs: no 64-bit division
-        return v.base + (int64_t)j * v.piece_stride + (int64_t)(t >> v.run_shift) * v.run_stride + (t & (v.run - 1));
-    return v.base + (int64_t)j * v.piece_stride + (int64_t)(t / v.run) * v.run_stride + (t % v.run);
+        return pb + (int64_t)(t >> v.run_shift) * v.run_stride + (t & (v.run - 1));
+    return pb + (int64_t)(t / v.run) * v.run_stride + (t % v.run);
 }
 
-// 64-byte block starting at byte t of piece j, `len` valid bytes (zero padded)
-template <bool kFast>
-__device__ __forceinline__ void load_block(const B3View &v, uint64_t j, uint64_t t, uint32_t len, uint32_t (&m)[16]) {
-    if (kFast && len == 64) {  // the block lies in one run, 16-byte aligned
-        const u32x4 *p = reinterpret_cast<const u32x4 *>(at<kFast>(v, j, t));
+// `n` 16-byte words at p (plain loads: the second half of each 128-byte
+// line is read by the next block, so non-temporal loads, which let the line
+// go, cost 2x here -- tools/exp/b3_probe.hip)
+template <int n>
+__device__ __forceinline__ void load_words(const uint8_t *p, uint32_t *m) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            u32x4 w = __builtin_nontemporal_load(p + q);
-            m[4 * q] = w[0], m[4 * q + 1] = w[1], m[4 * q + 2] = w[2], m[4 * q + 3] = w[3];
-        }
+    for (int i = 0; i < n; i++) {
+        u32x4 w = q[i];
+        m[4 * i] = w[0], m[4 * i + 1] = w[1], m[4 * i + 2] = w[2], m[4 * i + 3] = w[3];
+    }
+}
+
+// 64-byte block starting at byte t, `len` valid bytes (zero padded)
+template <bool kFast>
+__device__ __forceinline__ void load_block(const B3View &v, const uint8_t *pb, uint64_t t, uint32_t len,
+                                           uint32_t (&m)[16]) {
+    if (kFast && len == 64) {  // the block lies in one run, 16-byte aligned
+        load_words<4>(at<kFast>(v, pb, t), m);
         return;
     }
 #pragma unroll
     for (int i = 0; i < 16; i++) m[i] = 0;
-    for (uint32_t b = 0; b < len; b++) m[b >> 2] |= (uint32_t)*at<kFast>(v, j, t + b) << (8 * (b & 3));
+    for (uint32_t b = 0; b < len; b++) m[b >> 2] |= (uint32_t)*at<kFast>(v, pb, t + b) << (8 * (b & 3));
 }
 
-__device__ __forceinline__ void store_hash(uint8_t *out, const uint32_t (&h)[8]) {
-    uint4 *o = reinterpret_cast<uint4 *>(out);
-    o[0] = make_uint4(h[0], h[1], h[2], h[3]);
-    o[1] = make_uint4(h[4], h[5], h[6], h[7]);
+// CV of a full 1 KiB chunk whose 128-byte lines each lie in one run: one
+// whole line (two blocks) per load step, the next line in flight meanwhile
+__device__ __forceinline__ void full_chunk_lines(const B3View &v, const uint8_t *pb, uint64_t t0, uint64_t c,
+                                                 uint32_t last_flags, uint32_t (&h)[8]) {
+    uint32_t m[32], nx[32];
+    load_words<8>(at<true>(v, pb, t0), m);
+    for (int pr = 0; pr < 8; pr++) {
+        if (pr < 7) load_words<8>(at<true>(v, pb, t0 + 128 * (pr + 1)), nx);
+        uint32_t lo[16], hi[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) lo[i] = m[i], hi[i] = m[16 + i];
+        compress(h, lo, (uint32_t)c, (uint32_t)(c >> 32), 64, pr == 0 ? kChunkStart : 0);
+        compress(h, hi, (uint32_t)c, (uint32_t)(c >> 32), 64, pr == 7 ? last_flags : 0);
+#pragma unroll
+        for (int i = 0; i < 32; i++) m[i] = nx[i];
+    }
 }
 
-// Folds `cnt` nodes held in lds[0] (layout [word][kGroup]) into one.  If
-// `whole` (the nodes are every node of the piece), the last parent is the
-// root and the function returns with the hash in `out` of thread 0; else
-// thread 0 gets the subtree CV.  cnt >= 2 when whole.
-__device__ void fold(uint32_t (*lds)[8][kGroup], int cnt, bool whole, uint32_t (&out)[8]) {
-    const int t = threadIdx.x;
-    int cur = 0;
-    while (cnt > 1) {
-        const int pairs = cnt >> 1;
-        if (t < pairs) {
-            uint32_t l[8], r[8], h[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) l[i] = lds[cur][i][2 * t], r[i] = lds[cur][i][2 * t + 1];
-            parent(h, l, r, whole && cnt == 2);
-#pragma unroll
-            for (int i = 0; i < 8; i++) lds[cur ^ 1][i][t] = h[i];
-        } else if (t == pairs && (cnt & 1)) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) lds[cur ^ 1][i][t] = lds[cur][i][cnt - 1];
-        }
-        __syncthreads();
-        cnt = (cnt + 1) >> 1;
-        cur ^= 1;
-    }
-    if (t == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) out[i] = lds[cur][i][0];
-    }
-}
+// Two views of pieces with the same length hashed in one launch (the data
+// and the parity pieces of a batch of segments): piece p < split is piece p
+// of v[0], else piece p - split of v[1]; hashes and tree nodes are indexed
+// by p.
+struct B3Pair {
+    B3View v[2];
+    uint64_t split;
+};
 
 template <bool kFast>
-__global__ __launch_bounds__(kGroup) void b3_chunks(B3View v, uint64_t nchunks, uint32_t groups, uint32_t *nodes,
+__global__ __launch_bounds__(kGroup) void b3_chunks(B3Pair pv, uint64_t nchunks, uint32_t groups, uint32_t *nodes,
                                                      uint8_t *hashes) {
     __shared__ uint32_t lds[2][8][kGroup];
     const uint64_t piece = blockIdx.x / groups;
     const uint32_t group = blockIdx.x % groups;
     const uint64_t c = (uint64_t)group * kGroup + threadIdx.x;
     const bool single = nchunks == 1;
+    const bool second = piece >= pv.split;
+    const B3View &v = pv.v[second];
+    const uint8_t *pb = piece_base(v, second ? piece - pv.split : piece);
     if (c < nchunks) {
         const uint64_t t0 = c * 1024;
         const uint64_t clen = v.piece_len - t0 < 1024 ? v.piece_len - t0 : 1024;  // 0 only for an empty piece
-        const uint32_t nb = clen ? (uint32_t)((clen + 63) >> 6) : 1;
         uint32_t h[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) h[i] = kIV[i];
-        uint32_t m[16], nx[16];
-        load_block<kFast>(v, piece, t0, nb == 1 ? (uint32_t)clen : 64, m);
-        for (uint32_t b = 0; b < nb; b++) {
-            const bool last = b + 1 == nb;
-            const uint32_t blen = last ? (uint32_t)(clen - 64ull * b) : 64;
-            if (!last) {  // prefetch the next block while this one compresses
-                const uint32_t nlen = b + 2 == nb ? (uint32_t)(clen - 64ull * (b + 1)) : 64;
-                load_block<kFast>(v, piece, t0 + 64ull * (b + 1), nlen, nx);
-            }
-            const uint32_t flags = (b == 0 ? kChunkStart : 0) | (last ? kChunkEnd : 0) | (last && single ? kRoot : 0);
-            compress(h, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
-            if (!last) {
+        if (UPLINK_B3_LINES && kFast && clen == 1024 && v.run_shift >= 7) {
+            full_chunk_lines(v, pb, t0, c, kChunkEnd | (single ? kRoot : 0), h);
+        } else {  // partial chunk, 64-byte runs, or the byte path: block by block
+            const uint32_t nb = clen ? (uint32_t)((clen + 63) >> 6) : 1;
+            uint32_t m[16], nx[16];
+            load_block<kFast>(v, pb, t0, nb == 1 ? (uint32_t)clen : 64, m);
+            for (uint32_t b = 0; b < nb; b++) {
+                const bool last = b + 1 == nb;
+                const uint32_t blen = last ? (uint32_t)(clen - 64ull * b) : 64;
+                if (!last) {  // prefetch the next block while this one compresses
+                    const uint32_t nlen = b + 2 == nb ? (uint32_t)(clen - 64ull * (b + 1)) : 64;
+                    load_block<kFast>(v, pb, t0 + 64ull * (b + 1), nlen, nx);
+                }
+                const uint32_t flags =
+                    (b == 0 ? kChunkStart : 0) | (last ? kChunkEnd : 0) | (last && single ? kRoot : 0);
+                compress(h, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
+                if (!last) {
 #pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = nx[i];
+                    for (int i = 0; i < 16; i++) m[i] = nx[i];
+                }
             }
         }
         if (single) {
@@ -263,32 +207,47 @@ size_t b3_workspace_bytes(const B3View &v) {
     return (size_t)(v.npieces * (g1 + (g2 > 1 ? g2 : 0)) * 32);
 }
 
-hipError_t b3_launch(const B3View &view, uint8_t *hashes, void *ws, hipStream_t stream) {
-    if (view.npieces == 0) return hipSuccess;
-    if (!view.base && view.piece_len) return hipErrorInvalidValue;
+static B3View normalized(const B3View &view) {
     B3View v = view;
     if (v.run == 0 || v.run >= v.piece_len || v.run_stride == (int64_t)v.run) {  // contiguous pieces
         v.run = 1ull << 62;
         v.run_stride = 0;
     }
     v.run_shift = (v.run & (v.run - 1)) == 0 ? __builtin_ctzll(v.run) : -1;
-    const uint64_t nchunks = chunks_of(v);
+    if (v.pieces_per_set == 0 || v.pieces_per_set > v.npieces) {  // one set
+        v.pieces_per_set = v.npieces;
+        v.set_stride = 0;
+    }
+    return v;
+}
+
+static bool fast_ok(const B3View &v) {
+    return v.npieces == 0 || (v.run_shift >= 6 && (reinterpret_cast<uintptr_t>(v.base) & 15) == 0 &&
+                              (v.piece_stride & 15) == 0 && (v.run_stride & 15) == 0 && (v.set_stride & 15) == 0);
+}
+
+hipError_t b3_launch2(const B3View &first, const B3View &second, uint8_t *hashes, void *ws, hipStream_t stream) {
+    if (second.npieces && first.npieces && second.piece_len != first.piece_len) return hipErrorInvalidValue;
+    B3Pair pv{{normalized(first), normalized(second)}, first.npieces};
+    const uint64_t npieces = first.npieces + second.npieces;
+    if (npieces == 0) return hipSuccess;
+    for (const B3View &v : pv.v)
+        if (v.npieces && !v.base && v.piece_len) return hipErrorInvalidValue;
+    const uint64_t nchunks = chunks_of(first.npieces ? first : second);
     uint64_t groups = ceil_div(nchunks, kGroup);
-    if (groups > 0xFFFFFFFFull / kGroup || v.npieces * groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    const bool aligned = v.run_shift >= 6 && (reinterpret_cast<uintptr_t>(v.base) & 15) == 0 &&
-                         (v.piece_stride & 15) == 0 && (v.run_stride & 15) == 0;
+    if (groups > 0xFFFFFFFFull / kGroup || npieces * groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
     uint32_t *a = static_cast<uint32_t *>(ws);
-    uint32_t *b = groups > 1 ? a + v.npieces * groups * 8 : nullptr;
-    const dim3 grid((uint32_t)(v.npieces * groups));
-    if (aligned)
-        b3_chunks<true><<<grid, kGroup, 0, stream>>>(v, nchunks, (uint32_t)groups, a, hashes);
+    uint32_t *b = groups > 1 ? a + npieces * groups * 8 : nullptr;
+    const dim3 grid((uint32_t)(npieces * groups));
+    if (fast_ok(pv.v[0]) && fast_ok(pv.v[1]))
+        b3_chunks<true><<<grid, kGroup, 0, stream>>>(pv, nchunks, (uint32_t)groups, a, hashes);
     else
-        b3_chunks<false><<<grid, kGroup, 0, stream>>>(v, nchunks, (uint32_t)groups, a, hashes);
+        b3_chunks<false><<<grid, kGroup, 0, stream>>>(pv, nchunks, (uint32_t)groups, a, hashes);
     hipError_t e = hipGetLastError();
     while (e == hipSuccess && groups > 1) {
         const uint64_t next = ceil_div(groups, kGroup);
-        b3_parents<<<dim3((uint32_t)(v.npieces * next)), kGroup, 0, stream>>>(a, (uint32_t)groups, (uint32_t)next, b,
-                                                                            hashes);
+        b3_parents<<<dim3((uint32_t)(npieces * next)), kGroup, 0, stream>>>(a, (uint32_t)groups, (uint32_t)next, b,
+                                                                          hashes);
         e = hipGetLastError();
         groups = next;
         uint32_t *t = a;
@@ -296,6 +255,11 @@ hipError_t b3_launch(const B3View &view, uint8_t *hashes, void *ws, hipStream_t 
         b = t;
     }
     return e;
+}
+
+hipError_t b3_launch(const B3View &v, uint8_t *hashes, void *ws, hipStream_t stream) {
+    B3View none{};
+    return b3_launch2(v, none, hashes, ws, stream);
 }
 
 }  // namespace uplink_ec

@@ -8,8 +8,10 @@
 
 namespace uplink_ec {
 
-// npieces byte strings of piece_len bytes each.  Byte t of string j lives at
-//   base + j*piece_stride + (t / run)*run_stride + t % run
+// npieces byte strings of piece_len bytes each, in sets of pieces_per_set
+// (0 = one set).  Byte t of string j lives at
+//   base + (j / pieces_per_set)*set_stride + (j % pieces_per_set)*piece_stride
+//        + (t / run)*run_stride + t % run
 // (run = piece_len for contiguous pieces; run = ess, run_stride = k*ess for
 // the data pieces of a stripe-major segment).
 struct B3View {
@@ -19,6 +21,8 @@ struct B3View {
     uint64_t run;
     int64_t run_stride;
     uint64_t npieces;
+    uint64_t pieces_per_set;
+    int64_t set_stride;
     int32_t run_shift;  // set by b3_launch: log2(run) when run is a power of two, else -1
 };
 
@@ -28,5 +32,8 @@ size_t b3_workspace_bytes(const B3View &v);
 
 // hashes: npieces*32 bytes on the device.  `ws` has b3_workspace_bytes(v).
 hipError_t b3_launch(const B3View &v, uint8_t *hashes, void *ws, hipStream_t stream);
+// Both views in one launch (equal piece_len): hashes of `first`'s pieces,
+// then `second`'s.  ws: b3_workspace_bytes of a view with the summed npieces.
+hipError_t b3_launch2(const B3View &first, const B3View &second, uint8_t *hashes, void *ws, hipStream_t stream);
 
 }  // namespace uplink_ec

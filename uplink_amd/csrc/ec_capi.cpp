@@ -606,23 +606,36 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // are contiguous in `parity` ([n-k][plen]), data piece j is share j of every
 // stripe of the stripe-major segment `seg` (runs of ess bytes, k*ess apart).
 // hashes: n*32 device bytes; ws: b3_segment_ws_bytes.
-static B3View data_view(const ec_ctx *c, const uint8_t *seg, size_t nstripes) {
-    return B3View{seg, (int64_t)c->ess, nstripes * (uint64_t)c->ess, (uint64_t)c->ess, (int64_t)c->k * c->ess,
-                  (uint64_t)c->k, 0};
-}
-static B3View parity_view(const ec_ctx *c, const uint8_t *parity, size_t nstripes) {
+// hashes [nseg][n][32]: the data pieces of all nseg segments in one launch,
+// the parity pieces in another; the hash rows of a segment are n*32 apart,
+// so each launch writes into a [nseg][rows][32] staging area first.
+static B3View data_view(const ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes) {
     const uint64_t plen = nstripes * (uint64_t)c->ess;
-    return B3View{parity, (int64_t)plen, plen, plen, (int64_t)plen, (uint64_t)(c->n - c->k), 0};
+    return B3View{segs, (int64_t)c->ess, plen, (uint64_t)c->ess, (int64_t)c->k * c->ess, nseg * (uint64_t)c->k,
+                  (uint64_t)c->k, (int64_t)(plen * c->k), 0};
 }
-static size_t b3_segment_ws_bytes(const ec_ctx *c, size_t nstripes) {
-    return align_up(std::max(b3_workspace_bytes(data_view(c, nullptr, nstripes)),
-                             b3_workspace_bytes(parity_view(c, nullptr, nstripes))),
-                    256);
+static B3View parity_view(const ec_ctx *c, const uint8_t *parity, size_t nseg, size_t nstripes) {
+    const uint64_t plen = nstripes * (uint64_t)c->ess;
+    return B3View{parity, (int64_t)plen, plen, plen, (int64_t)plen, nseg * (uint64_t)(c->n - c->k), 0, 0, 0};
 }
-static int hash_segment(const ec_ctx *c, const uint8_t *seg, const uint8_t *parity, size_t nstripes, uint8_t *hashes,
-                        uint8_t *ws, hipStream_t st) {
-    HIP_TRY(b3_launch(data_view(c, seg, nstripes), hashes, ws, st));
-    if (c->n > c->k) HIP_TRY(b3_launch(parity_view(c, parity, nstripes), hashes + 32 * (size_t)c->k, ws, st));
+static size_t b3_segment_ws_bytes(const ec_ctx *c, size_t nseg, size_t nstripes) {
+    B3View all = parity_view(c, nullptr, nseg, nstripes);
+    all.npieces = nseg * (uint64_t)c->n;
+    return align_up(b3_workspace_bytes(all), 256) + align_up(32 * nseg * (size_t)c->n, 256);
+}
+static int hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,
+                         uint8_t *hashes, uint8_t *ws, hipStream_t st) {
+    const size_t n = c->n, k = c->k;
+    uint8_t *stage = ws;  // [data: nseg*k*32][parity: nseg*(n-k)*32]
+    uint8_t *tree = ws + align_up(32 * nseg * n, 256);
+    B3View pv = parity_view(c, parity, nseg, nstripes);
+    if (n == k) pv.npieces = 0;
+    HIP_TRY(b3_launch2(data_view(c, segs, nseg, nstripes), pv, stage, tree, st));
+    // interleave to [nseg][n][32]
+    HIP_TRY(hipMemcpy2DAsync(hashes, 32 * n, stage, 32 * k, 32 * k, nseg, hipMemcpyDeviceToDevice, st));
+    if (n > k)
+        HIP_TRY(hipMemcpy2DAsync(hashes + 32 * k, 32 * n, stage + 32 * nseg * k, 32 * (n - k), 32 * (n - k), nseg,
+                                 hipMemcpyDeviceToDevice, st));
     return EC_OK;
 }
 
@@ -636,7 +649,7 @@ static int encode_host(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstri
     const size_t pbytes = (size_t)rows * nstripes * c->ess;
     // device slot: pieces | hashes (n*32) | BLAKE3 workspace
     const size_t hash_at = align_up(pbytes, 256), ws_at = hash_at + align_up(32 * (size_t)c->n, 256);
-    const size_t out_cap = hashes ? ws_at + b3_segment_ws_bytes(c, nstripes) : pbytes;
+    const size_t out_cap = hashes ? ws_at + b3_segment_ws_bytes(c, 1, nstripes) : pbytes;
     std::lock_guard<std::mutex> g(c->pipe_mu);
     int rc = pipe_reserve(c, spad, out_cap);
     if (rc) return rc;
@@ -652,7 +665,7 @@ static int encode_host(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstri
         if (rc) break;
         if (hashes) {
             const uint8_t *parity = d_out + (parity_only ? 0 : (size_t)c->k * nstripes * c->ess);
-            rc = hash_segment(c, c->pipe.d_in[slot], parity, nstripes, d_out + hash_at, d_out + ws_at, st);
+            rc = hash_segments(c, c->pipe.d_in[slot], parity, 1, nstripes, d_out + hash_at, d_out + ws_at, st);
             if (rc) break;
             if (hipMemcpyAsync(hashes + s * 32 * (size_t)c->n, d_out + hash_at, 32 * (size_t)c->n,
                                hipMemcpyDeviceToHost, st) != hipSuccess) {
@@ -682,15 +695,10 @@ int ec_hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity
     if (!c || !segs || !hashes || (c->n > c->k && !parity)) return EC_ERR_INVALID_ARG;
     if (nseg == 0) return EC_OK;
     hipStream_t st = (hipStream_t)stream;
-    const size_t ws_bytes = b3_segment_ws_bytes(c, nstripes);
     void *ws = nullptr;
-    if (ws_bytes) HIP_TRY(hipMallocAsync(&ws, ws_bytes, st));
-    int rc = EC_OK;
-    const size_t spad = nstripes * (size_t)c->k * c->ess, pbytes = (size_t)(c->n - c->k) * nstripes * c->ess;
-    for (size_t s = 0; s < nseg && rc == EC_OK; s++)
-        rc = hash_segment(c, segs + s * spad, parity ? parity + s * pbytes : nullptr, nstripes,
-                          hashes + s * 32 * (size_t)c->n, (uint8_t *)ws, st);
-    if (ws) (void)hipFreeAsync(ws, st);
+    HIP_TRY(hipMallocAsync(&ws, b3_segment_ws_bytes(c, nseg, nstripes), st));
+    const int rc = hash_segments(c, segs, parity, nseg, nstripes, hashes, (uint8_t *)ws, st);
+    (void)hipFreeAsync(ws, st);
     return rc;
 }
 
@@ -699,7 +707,7 @@ int ec_blake3_pieces(const uint8_t *base, size_t npieces, long long piece_stride
     if (!hashes || (!base && piece_len && npieces)) return EC_ERR_INVALID_ARG;
     if (npieces == 0) return EC_OK;
     hipStream_t st = (hipStream_t)stream;
-    const B3View v{base, piece_stride, piece_len, run, run_stride, npieces, 0};
+    const B3View v{base, piece_stride, piece_len, run, run_stride, npieces, 0, 0, 0};
     const size_t ws_bytes = b3_workspace_bytes(v);
     void *ws = nullptr;
     if (ws_bytes) HIP_TRY(hipMallocAsync(&ws, ws_bytes, st));
