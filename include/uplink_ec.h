@@ -29,6 +29,8 @@
  *   ec_*blake3* / ec_hash_segments / ec_encode_segments_host_hashed
  *                            BLAKE3 piece hash of the upload (piecestore/upload.go:
  *                            133,155,270; hash.go:20-26), SURVEY §8f row 4
+ *   ec_gcm_*                 AES-256-GCM segment encryption: splitter/splitter.go:156,170
+ *                            (upload), streams/store.go:347-382 (download), SURVEY §8f row 4
  *   ec_strerror/ec_format_error  error texts of infectious / eestream
  *
  * Error codes map to the errors eestream's callers test:
@@ -68,6 +70,7 @@ extern "C" {
 #define EC_ERR_DEVICE (-11)           /* HIP runtime error or no GPU */
 #define EC_ERR_UNSUPPORTED (-12)      /* outside the engine's limits */
 #define EC_ERR_SHARE_SIZE (-13)       /* shares of different lengths */
+#define EC_ERR_AUTH (-14)             /* "cipher: message authentication failed" (a GCM tag did not verify) */
 
 /* flags for ec_encode_segments */
 #define EC_FLAG_PARITY_ONLY 0x1 /* write only the n-k parity pieces */
@@ -165,6 +168,36 @@ int ec_hash_segments(const ec_ctx *ctx, const uint8_t *segs, const uint8_t *pari
                      uint8_t *hashes, ec_stream stream);
 /* Host buffers, synchronous: hashes[32*j] = BLAKE3(data + j*stride, piece_len) */
 int ec_blake3_host(const uint8_t *data, size_t npieces, long long stride, size_t piece_len, uint8_t *hashes);
+
+/* ---- AES-256-GCM segment encryption (storj.io/common/encryption, EncAESGCM) ----
+ * Replace encryption.TransformWriterPadded(buf, NewEncrypter(EncAESGCM, key,
+ * nonce, BlockSize)) on upload (splitter/splitter.go:156,170) and
+ * Transform(rr, NewDecrypter(...)) on download (streams/store.go:354-377):
+ * blocks of in_block = BlockSize - 16 plaintext bytes (7408 for BlockSize
+ * 29*256, project.go:84), block b sealed under the 12-byte nonce + b
+ * (little-endian increment, as calcGCMNonce), written as ciphertext || tag.
+ * Padding of the plaintext (PadReader rule) and Unpad are the caller's.
+ * in_block must be a multiple of 16, buffers 16-byte aligned. */
+
+/* device bytes of one prepared key */
+size_t ec_gcm_key_bytes(void);
+/* expands nkeys 32-byte keys (host) into dev_keys (nkeys * ec_gcm_key_bytes()
+ * device bytes): round keys + GHASH tables; synchronous */
+int ec_gcm_prepare_keys(const uint8_t *keys, size_t nkeys, void *dev_keys, ec_stream stream);
+/* plain: [nseg][nblocks*in_block] -> out: [nseg][nblocks*(in_block+16)];
+ * segment g uses prepared key g and nonce dev_nonces[12*g..]; async */
+int ec_gcm_seal_segments(const uint8_t *plain, size_t nseg, size_t nblocks, size_t in_block, const void *dev_keys,
+                         const uint8_t *dev_nonces, uint8_t *out, ec_stream stream);
+/* the inverse; dev_status[g] = -1 when every block of segment g verified,
+ * else the first block whose tag did not (its plaintext must not be used) */
+int ec_gcm_open_segments(const uint8_t *cipher, size_t nseg, size_t nblocks, size_t in_block, const void *dev_keys,
+                         const uint8_t *dev_nonces, uint8_t *out, int32_t *dev_status, ec_stream stream);
+/* host buffers, one segment, synchronous; open returns EC_ERR_AUTH and the
+ * first failing block in *bad_block when a tag does not verify */
+int ec_gcm_seal_host(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *plain, size_t nblocks,
+                     size_t in_block, uint8_t *out);
+int ec_gcm_open_host(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *cipher, size_t nblocks,
+                     size_t in_block, uint8_t *out, long long *bad_block);
 
 /* ---- device helpers ---- */
 int ec_device_count(void);

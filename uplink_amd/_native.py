@@ -26,6 +26,7 @@ EC_ERR_INVALID_ARG = -10
 EC_ERR_DEVICE = -11
 EC_ERR_UNSUPPORTED = -12
 EC_ERR_SHARE_SIZE = -13
+EC_ERR_AUTH = -14
 
 EC_FLAG_PARITY_ONLY = 0x1
 
@@ -64,6 +65,14 @@ SIGNATURES = {
                                         ctypes.c_longlong, vp, vp]),
     "ec_hash_segments": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, vp]),
     "ec_blake3_host": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_size_t, vp]),
+    "ec_gcm_key_bytes": (ctypes.c_size_t, []),
+    "ec_gcm_prepare_keys": (ctypes.c_int, [vp, ctypes.c_size_t, vp, vp]),
+    "ec_gcm_seal_segments": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, vp, vp, vp, vp]),
+    "ec_gcm_open_segments": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, vp, vp, vp, vp,
+                                            vp]),
+    "ec_gcm_seal_host": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp]),
+    "ec_gcm_open_host": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp,
+                                        ctypes.POINTER(ctypes.c_longlong)]),
     "ec_host_alloc": (vp, [ctypes.c_size_t]),
     "ec_host_free": (None, [vp]),
     "ec_device_count": (ctypes.c_int, []),

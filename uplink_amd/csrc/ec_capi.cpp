@@ -337,6 +337,7 @@ const char *ec_strerror(int code) {
         case EC_ERR_DEVICE: return "HIP device error";
         case EC_ERR_UNSUPPORTED: return "unsupported parameters";
         case EC_ERR_SHARE_SIZE: return "shares must all have the same length";
+        case EC_ERR_AUTH: return "cipher: message authentication failed";
         default: return "unknown error";
     }
 }
