@@ -71,12 +71,15 @@ def open_(key: bytes, nonce12: bytes, sealed: bytes) -> bytes | None:
     return out[:n].tobytes() if rc == 0 else None
 
 
-def encrypt_blocks(key: bytes, nonce: bytes, padded: np.ndarray, in_block: int, threads: int = 1) -> np.ndarray:
-    """Encrypter.Transform over the padded plaintext: [nblocks][in_block+16]."""
+def encrypt_blocks(key: bytes, nonce: bytes, padded: np.ndarray, in_block: int, threads: int = 1,
+                   out: np.ndarray | None = None) -> np.ndarray:
+    """Encrypter.Transform over the padded plaintext: [nblocks][in_block+16]
+    (into `out` when given, e.g. a pre-faulted buffer for timing)."""
     padded = np.ascontiguousarray(padded, dtype=np.uint8).reshape(-1)
     nb = padded.size // in_block
     assert nb * in_block == padded.size
-    out = np.empty((nb, in_block + TAG), dtype=np.uint8)
+    if out is None:
+        out = np.empty((nb, in_block + TAG), dtype=np.uint8)
     rc = lib().ag_encrypt_blocks(key, nonce[:12], padded.ctypes.data, nb, in_block, out.ctypes.data, threads)
     assert rc == -1, rc
     return out

@@ -81,20 +81,43 @@ typedef struct {
     int64_t first_bad;
 } ag_job;
 
+/* one AEAD per worker, as the reference keeps one cipher.AEAD per segment
+ * (NewAESGCMEncrypter); per block only the nonce changes */
 static void *ag_worker(void *a) {
     ag_job *j = (ag_job *)a;
     const size_t ob = j->in_block + 16;
-    for (size_t b = j->first; b < j->first + j->count; b++) {
+    EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
+    int ok = c && (j->open ? EVP_DecryptInit_ex(c, EVP_aes_256_gcm(), NULL, NULL, NULL)
+                           : EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), NULL, NULL, NULL)) &&
+             EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 12, NULL) &&
+             (j->open ? EVP_DecryptInit_ex(c, NULL, NULL, j->key, NULL) : EVP_EncryptInit_ex(c, NULL, NULL, j->key, NULL));
+    for (size_t b = j->first; ok && b < j->first + j->count; b++) {
         uint8_t nonce[12];
         memcpy(nonce, j->nonce, 12);
         ag_increment(nonce, 12, b);
-        int rc = j->open ? ag_open(j->key, nonce, j->in + b * ob, j->in_block, j->out + b * j->in_block)
-                         : ag_seal(j->key, nonce, NULL, 0, j->in + b * j->in_block, j->in_block, j->out + b * ob);
-        if (rc && !j->failed) {
+        int n = 0, f = 0, good;
+        if (j->open) {
+            const uint8_t *in = j->in + b * ob;
+            uint8_t *out = j->out + b * j->in_block;
+            good = EVP_DecryptInit_ex(c, NULL, NULL, NULL, nonce) && EVP_DecryptUpdate(c, out, &n, in, (int)j->in_block) &&
+                   EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, (void *)(in + j->in_block)) &&
+                   EVP_DecryptFinal_ex(c, out + n, &f) > 0;
+        } else {
+            const uint8_t *in = j->in + b * j->in_block;
+            uint8_t *out = j->out + b * ob;
+            good = EVP_EncryptInit_ex(c, NULL, NULL, NULL, nonce) && EVP_EncryptUpdate(c, out, &n, in, (int)j->in_block) &&
+                   EVP_EncryptFinal_ex(c, out + n, &f) && EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, out + j->in_block);
+        }
+        if (!good && !j->failed) {
             j->failed = 1;
             j->first_bad = (int64_t)b;
         }
     }
+    if (!ok && !j->failed) {
+        j->failed = 1;
+        j->first_bad = (int64_t)j->first;
+    }
+    EVP_CIPHER_CTX_free(c);
     return NULL;
 }
 
