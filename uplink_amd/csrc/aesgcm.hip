@@ -86,32 +86,53 @@ __device__ constexpr uint32_t kRem4[16] = {0x0000u << 16, 0x1C20u << 16, 0x3840u
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
 
+// T-table layout.  kCopies = 0: T0..T3 once each (4 KB; random lanes collide
+// on LDS banks).  kCopies = C > 0: T0 alone, replicated C times with copy c of
+// entry x at word x*C + c, lane l reading copy l % C, so lanes read distinct
+// banks (C = 64) or at most two share one (C = 32); T1..T3 are rotations.
+#ifndef UPLINK_GCM_COPIES
+#define UPLINK_GCM_COPIES 32
+#endif
+constexpr int kCopies = UPLINK_GCM_COPIES;
+
 struct Lds {
-    uint32_t t[4][256];          // T0..T3
+    uint32_t t[kCopies ? 256 * kCopies : 4 * 256];
     uint32_t rem[16];
     uint32_t htab[64][16][4];    // H^1..H^64
 };
 
+// Tk[x] for this lane
+template <int k>
+__device__ __forceinline__ uint32_t T(const Lds &L, uint32_t x, uint32_t copy) {
+    if constexpr (kCopies == 0) {
+        return L.t[k * 256 + x];
+    } else {
+        const uint32_t v = L.t[x * kCopies + copy];
+        return k ? __builtin_amdgcn_alignbit(v, v, 8 * k) : v;
+    }
+}
+
 // AES-256 of the big-endian words s[4] with round keys rk (SGPRs), T-tables in LDS
 __device__ __forceinline__ void aes_encrypt(uint32_t (&s)[4], const uint32_t *__restrict__ rk, const Lds &L) {
+    const uint32_t cp = kCopies ? threadIdx.x % (kCopies ? kCopies : 1) : 0;
     uint32_t a = s[0] ^ rk[0], b = s[1] ^ rk[1], c = s[2] ^ rk[2], d = s[3] ^ rk[3];
 #pragma unroll
     for (int r = 1; r < 14; r++) {
-        const uint32_t e = L.t[0][a >> 24] ^ L.t[1][(b >> 16) & 255] ^ L.t[2][(c >> 8) & 255] ^ L.t[3][d & 255] ^ rk[4 * r];
-        const uint32_t f = L.t[0][b >> 24] ^ L.t[1][(c >> 16) & 255] ^ L.t[2][(d >> 8) & 255] ^ L.t[3][a & 255] ^ rk[4 * r + 1];
-        const uint32_t g = L.t[0][c >> 24] ^ L.t[1][(d >> 16) & 255] ^ L.t[2][(a >> 8) & 255] ^ L.t[3][b & 255] ^ rk[4 * r + 2];
-        const uint32_t h = L.t[0][d >> 24] ^ L.t[1][(a >> 16) & 255] ^ L.t[2][(b >> 8) & 255] ^ L.t[3][c & 255] ^ rk[4 * r + 3];
+        const uint32_t e = T<0>(L, a >> 24, cp) ^ T<1>(L, (b >> 16) & 255, cp) ^ T<2>(L, (c >> 8) & 255, cp) ^ T<3>(L, d & 255, cp) ^ rk[4 * r];
+        const uint32_t f = T<0>(L, b >> 24, cp) ^ T<1>(L, (c >> 16) & 255, cp) ^ T<2>(L, (d >> 8) & 255, cp) ^ T<3>(L, a & 255, cp) ^ rk[4 * r + 1];
+        const uint32_t g = T<0>(L, c >> 24, cp) ^ T<1>(L, (d >> 16) & 255, cp) ^ T<2>(L, (a >> 8) & 255, cp) ^ T<3>(L, b & 255, cp) ^ rk[4 * r + 2];
+        const uint32_t h = T<0>(L, d >> 24, cp) ^ T<1>(L, (a >> 16) & 255, cp) ^ T<2>(L, (b >> 8) & 255, cp) ^ T<3>(L, c & 255, cp) ^ rk[4 * r + 3];
         a = e, b = f, c = g, d = h;
     }
     // last round: S-box bytes, picked out of the T-tables (T2 MSB, T3 byte 2, T0 byte 1, T1 LSB = S[x])
-    s[0] = ((L.t[2][a >> 24] & 0xff000000u) | (L.t[3][(b >> 16) & 255] & 0x00ff0000u) |
-            (L.t[0][(c >> 8) & 255] & 0x0000ff00u) | (L.t[1][d & 255] & 0xffu)) ^ rk[56];
-    s[1] = ((L.t[2][b >> 24] & 0xff000000u) | (L.t[3][(c >> 16) & 255] & 0x00ff0000u) |
-            (L.t[0][(d >> 8) & 255] & 0x0000ff00u) | (L.t[1][a & 255] & 0xffu)) ^ rk[57];
-    s[2] = ((L.t[2][c >> 24] & 0xff000000u) | (L.t[3][(d >> 16) & 255] & 0x00ff0000u) |
-            (L.t[0][(a >> 8) & 255] & 0x0000ff00u) | (L.t[1][b & 255] & 0xffu)) ^ rk[58];
-    s[3] = ((L.t[2][d >> 24] & 0xff000000u) | (L.t[3][(a >> 16) & 255] & 0x00ff0000u) |
-            (L.t[0][(b >> 8) & 255] & 0x0000ff00u) | (L.t[1][c & 255] & 0xffu)) ^ rk[59];
+    s[0] = ((T<2>(L, a >> 24, cp) & 0xff000000u) | (T<3>(L, (b >> 16) & 255, cp) & 0x00ff0000u) |
+            (T<0>(L, (c >> 8) & 255, cp) & 0x0000ff00u) | (T<1>(L, d & 255, cp) & 0xffu)) ^ rk[56];
+    s[1] = ((T<2>(L, b >> 24, cp) & 0xff000000u) | (T<3>(L, (c >> 16) & 255, cp) & 0x00ff0000u) |
+            (T<0>(L, (d >> 8) & 255, cp) & 0x0000ff00u) | (T<1>(L, a & 255, cp) & 0xffu)) ^ rk[57];
+    s[2] = ((T<2>(L, c >> 24, cp) & 0xff000000u) | (T<3>(L, (d >> 16) & 255, cp) & 0x00ff0000u) |
+            (T<0>(L, (a >> 8) & 255, cp) & 0x0000ff00u) | (T<1>(L, b & 255, cp) & 0xffu)) ^ rk[58];
+    s[3] = ((T<2>(L, d >> 24, cp) & 0xff000000u) | (T<3>(L, (a >> 16) & 255, cp) & 0x00ff0000u) |
+            (T<0>(L, (b >> 8) & 255, cp) & 0x0000ff00u) | (T<1>(L, c & 255, cp) & 0xffu)) ^ rk[59];
 }
 
 // z = x * E in GF(2^128) (GCM bit order), E given by its 4-bit table; words big-endian
@@ -149,9 +170,13 @@ __global__ __launch_bounds__(256) void gcm_blocks(GcmBatch a, uint32_t wgs_per_s
     const uint32_t seg = blockIdx.x / wgs_per_seg;
     const uint32_t wg = blockIdx.x % wgs_per_seg;
     const GcmSched *ks = a.sched + seg;
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        const uint32_t t0 = kAesDev.t0[i];
-        L.t[0][i] = t0, L.t[1][i] = ror32(t0, 8), L.t[2][i] = ror32(t0, 16), L.t[3][i] = ror32(t0, 24);
+    if constexpr (kCopies == 0) {
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+            const uint32_t t0 = kAesDev.t0[i];
+            L.t[i] = t0, L.t[256 + i] = ror32(t0, 8), L.t[512 + i] = ror32(t0, 16), L.t[768 + i] = ror32(t0, 24);
+        }
+    } else {
+        for (int i = threadIdx.x; i < 256 * kCopies; i += blockDim.x) L.t[i] = kAesDev.t0[i / (kCopies ? kCopies : 1)];
     }
     if (threadIdx.x < 16) L.rem[threadIdx.x] = kRem4[threadIdx.x];
     {
