@@ -192,6 +192,19 @@ int ec_gcm_seal_segments(const uint8_t *plain, size_t nseg, size_t nblocks, size
  * else the first block whose tag did not (its plaintext must not be used) */
 int ec_gcm_open_segments(const uint8_t *cipher, size_t nseg, size_t nblocks, size_t in_block, const void *dev_keys,
                          const uint8_t *dev_nonces, uint8_t *out, int32_t *dev_status, ec_stream stream);
+/* the same with explicit segment strides in bytes (multiples of 16, at least
+ * the dense size), e.g. to seal straight into the RS encoder's padded input */
+int ec_gcm_seal_segments_strided(const uint8_t *plain, long long plain_seg_stride, size_t nseg, size_t nblocks,
+                                 size_t in_block, const void *dev_keys, const uint8_t *dev_nonces, uint8_t *out,
+                                 long long out_seg_stride, ec_stream stream);
+int ec_gcm_open_segments_strided(const uint8_t *cipher, long long cipher_seg_stride, size_t nseg, size_t nblocks,
+                                 size_t in_block, const void *dev_keys, const uint8_t *dev_nonces, uint8_t *out,
+                                 long long out_seg_stride, int32_t *dev_status, ec_stream stream);
+/* PadReader padding (single.go:236) on the device: after
+ * data_len bytes of each of nseg segments (seg_stride apart) write
+ * p = 4 + (block - (data_len+4) % block) % block bytes of byte(p), the last
+ * four the big-endian uint32 p.  Async on stream. */
+int ec_pad_segments(uint8_t *segs, size_t nseg, long long seg_stride, size_t data_len, size_t block, ec_stream stream);
 /* host buffers, one segment, synchronous; open returns EC_ERR_AUTH and the
  * first failing block in *bad_block when a tag does not verify */
 int ec_gcm_seal_host(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *plain, size_t nblocks,

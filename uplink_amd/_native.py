@@ -70,6 +70,11 @@ SIGNATURES = {
     "ec_gcm_seal_segments": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, vp, vp, vp, vp]),
     "ec_gcm_open_segments": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, vp, vp, vp, vp,
                                             vp]),
+    "ec_gcm_seal_segments_strided": (ctypes.c_int, [vp, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_size_t,
+                                                    ctypes.c_size_t, vp, vp, vp, ctypes.c_longlong, vp]),
+    "ec_gcm_open_segments_strided": (ctypes.c_int, [vp, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_size_t,
+                                                    ctypes.c_size_t, vp, vp, vp, ctypes.c_longlong, vp, vp]),
+    "ec_pad_segments": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_size_t, vp]),
     "ec_gcm_seal_host": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp]),
     "ec_gcm_open_host": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp,
                                         ctypes.POINTER(ctypes.c_longlong)]),
@@ -92,6 +97,15 @@ def load(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process.  PyTorch ships its own libamdhip64.so with
+    # the same soname (libamdhip64.so.7) as /opt/rocm's; when torch is loaded
+    # first this library binds to that copy.  Loaded the other way round, the
+    # process ends up with two runtimes and, once ours has made a HIP call,
+    # torch.cuda.is_available() returns False.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise NativeLibraryMissing(
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")

@@ -436,10 +436,19 @@ __global__ void gcm_status_fini(int32_t *s, uint32_t n) {
     if (i < n && s[i] == 0x7fffffff) s[i] = -1;
 }
 
+// PadReader padding written in place after `len` bytes of each segment
+__global__ void pad_segments(uint8_t *segs, int64_t stride, uint64_t len, uint32_t p) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p) return;
+    uint8_t v = (uint8_t)p;
+    if (i + 4 >= p) v = (uint8_t)(p >> (8 * (p - 1 - i)));  // last 4 bytes: big-endian p
+    segs[(int64_t)blockIdx.y * stride + len + i] = v;
+}
+
 int gcm_fail(hipError_t e) { return e == hipSuccess ? EC_OK : (e == hipErrorInvalidValue ? EC_ERR_INVALID_ARG : EC_ERR_DEVICE); }
 
 int gcm_run(const uint8_t *in, size_t nseg, size_t nblocks, size_t in_block, const void *keys, const uint8_t *nonces,
-            uint8_t *out, int32_t *status, bool open, hipStream_t st) {
+            uint8_t *out, int32_t *status, bool open, hipStream_t st, int64_t in_seg = 0, int64_t out_seg = 0) {
     if (nseg == 0 || nblocks == 0) return EC_OK;
     if (!in || !out || !keys || !nonces || (open && !status)) return EC_ERR_INVALID_ARG;
     if (in_block == 0 || in_block > (1u << 24) || nseg > 0xFFFFFFu || nblocks > 0x7FFFFFFFu) return EC_ERR_UNSUPPORTED;
@@ -449,8 +458,11 @@ int gcm_run(const uint8_t *in, size_t nseg, size_t nblocks, size_t in_block, con
     b.out = out;
     b.in_blk_stride = open ? ob : (int64_t)in_block;
     b.out_blk_stride = open ? (int64_t)in_block : ob;
-    b.in_seg_stride = b.in_blk_stride * (int64_t)nblocks;
-    b.out_seg_stride = b.out_blk_stride * (int64_t)nblocks;
+    b.in_seg_stride = in_seg ? in_seg : b.in_blk_stride * (int64_t)nblocks;
+    b.out_seg_stride = out_seg ? out_seg : b.out_blk_stride * (int64_t)nblocks;
+    if (b.in_seg_stride < b.in_blk_stride * (int64_t)nblocks || b.out_seg_stride < b.out_blk_stride * (int64_t)nblocks ||
+        ((b.in_seg_stride | b.out_seg_stride) & 15))
+        return EC_ERR_INVALID_ARG;
     b.sched = static_cast<const GcmSched *>(keys);
     b.nonces = nonces;
     b.status = status;
@@ -503,6 +515,20 @@ int ec_gcm_seal_segments(const uint8_t *plain, size_t nseg, size_t nblocks, size
     return gcm_run(plain, nseg, nblocks, in_block, dev_keys, dev_nonces, out, nullptr, false, (hipStream_t)stream);
 }
 
+int ec_gcm_seal_segments_strided(const uint8_t *plain, long long plain_seg_stride, size_t nseg, size_t nblocks,
+                                 size_t in_block, const void *dev_keys, const uint8_t *dev_nonces, uint8_t *out,
+                                 long long out_seg_stride, ec_stream stream) {
+    return gcm_run(plain, nseg, nblocks, in_block, dev_keys, dev_nonces, out, nullptr, false, (hipStream_t)stream,
+                   plain_seg_stride, out_seg_stride);
+}
+
+int ec_gcm_open_segments_strided(const uint8_t *cipher, long long cipher_seg_stride, size_t nseg, size_t nblocks,
+                                 size_t in_block, const void *dev_keys, const uint8_t *dev_nonces, uint8_t *out,
+                                 long long out_seg_stride, int32_t *dev_status, ec_stream stream) {
+    return gcm_run(cipher, nseg, nblocks, in_block, dev_keys, dev_nonces, out, dev_status, true, (hipStream_t)stream,
+                   cipher_seg_stride, out_seg_stride);
+}
+
 int ec_gcm_open_segments(const uint8_t *cipher, size_t nseg, size_t nblocks, size_t in_block, const void *dev_keys,
                          const uint8_t *dev_nonces, uint8_t *out, int32_t *dev_status, ec_stream stream) {
     return gcm_run(cipher, nseg, nblocks, in_block, dev_keys, dev_nonces, out, dev_status, true, (hipStream_t)stream);
@@ -543,6 +569,16 @@ static int gcm_host(const uint8_t key[32], const uint8_t nonce[12], const uint8_
     if (d) (void)hipFree(d);
     if (st) (void)hipStreamDestroy(st);
     return rc;
+}
+
+int ec_pad_segments(uint8_t *segs, size_t nseg, long long seg_stride, size_t data_len, size_t block, ec_stream stream) {
+    if (nseg == 0) return EC_OK;
+    if (!segs || block == 0 || nseg > 65535) return EC_ERR_INVALID_ARG;
+    const uint64_t p = 4 + (block - (data_len + 4) % block) % block;
+    if ((long long)(data_len + p) > seg_stride && nseg > 1) return EC_ERR_INVALID_ARG;
+    pad_segments<<<dim3((unsigned)((p + 255) / 256), (unsigned)nseg), 256, 0, (hipStream_t)stream>>>(
+        segs, seg_stride, data_len, (uint32_t)p);
+    return gcm_fail(hipGetLastError());
 }
 
 int ec_gcm_seal_host(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *plain, size_t nblocks,
