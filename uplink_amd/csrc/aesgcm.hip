@@ -76,7 +76,7 @@ struct AesTables {
 constexpr AesTables kAes{};
 __device__ constexpr AesTables kAesDev{};
 
-constexpr uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+constexpr uint32_t ror32(uint32_t x, int n) { return n ? (x >> n) | (x << (32 - n)) : x; }
 
 // Shoup's reduction constants for a 4-bit shift, placed at the top of word 0
 __device__ constexpr uint32_t kRem4[16] = {0x0000u << 16, 0x1C20u << 16, 0x3840u << 16, 0x2460u << 16,
@@ -90,13 +90,22 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_amdgcn_
 // on LDS banks).  kCopies = C > 0: T0 alone, replicated C times with copy c of
 // entry x at word x*C + c, lane l reading copy l % C, so lanes read distinct
 // banks (C = 64) or at most two share one (C = 32); T1..T3 are rotations.
+// experiment switch (tools/exp/gcm_var.cpp): 1 = skip the GHASH Horner multiplies,
+// 2 = skip the AES rounds; results are then wrong
+#ifndef UPLINK_GCM_EXP
+#define UPLINK_GCM_EXP 0
+#endif
 #ifndef UPLINK_GCM_COPIES
 #define UPLINK_GCM_COPIES 32
 #endif
+#ifndef UPLINK_GCM_TABLES
+#define UPLINK_GCM_TABLES 1
+#endif
 constexpr int kCopies = UPLINK_GCM_COPIES;
+constexpr int kTables = UPLINK_GCM_TABLES;  // 1: T0 only, T1..T3 by rotation; 4: all four stored
 
 struct Lds {
-    uint32_t t[kCopies ? 256 * kCopies : 4 * 256];
+    uint32_t t[kCopies ? kTables * 256 * kCopies : 4 * 256];
     uint32_t rem[16];
     uint32_t htab[64][16][4];    // H^1..H^64
 };
@@ -106,6 +115,8 @@ template <int k>
 __device__ __forceinline__ uint32_t T(const Lds &L, uint32_t x, uint32_t copy) {
     if constexpr (kCopies == 0) {
         return L.t[k * 256 + x];
+    } else if constexpr (kTables == 4) {
+        return L.t[(k * 256 + x) * kCopies + copy];
     } else {
         const uint32_t v = L.t[x * kCopies + copy];
         return k ? __builtin_amdgcn_alignbit(v, v, 8 * k) : v;
@@ -176,7 +187,10 @@ __global__ __launch_bounds__(256) void gcm_blocks(GcmBatch a, uint32_t wgs_per_s
             L.t[i] = t0, L.t[256 + i] = ror32(t0, 8), L.t[512 + i] = ror32(t0, 16), L.t[768 + i] = ror32(t0, 24);
         }
     } else {
-        for (int i = threadIdx.x; i < 256 * kCopies; i += blockDim.x) L.t[i] = kAesDev.t0[i / (kCopies ? kCopies : 1)];
+        for (int i = threadIdx.x; i < kTables * 256 * kCopies; i += blockDim.x) {
+            const int e = i / (kCopies ? kCopies : 1);  // table * 256 + entry
+            L.t[i] = ror32(kAesDev.t0[e & 255], 8 * (e >> 8));
+        }
     }
     if (threadIdx.x < 16) L.rem[threadIdx.x] = kRem4[threadIdx.x];
     {
@@ -224,7 +238,7 @@ __global__ __launch_bounds__(256) void gcm_blocks(GcmBatch a, uint32_t wgs_per_s
             // every lane runs the AES (no divergent second pass): data lanes on their counter block,
             // padding lanes on J0 (the tag mask), the length-block lane on a value it ignores
             uint32_t ks4[4] = {j0w0, j0w1, j0w2, is_data ? 2 + sidx : 1};
-            aes_encrypt(ks4, rk, L);
+            if (UPLINK_GCM_EXP != 2) aes_encrypt(ks4, rk, L);
             uint32_t y[4] = {0, 0, 0, 0};
             if (is_data) {
                 const uint32_t n = (sidx + 1 == nsub && tail) ? tail : 16;
@@ -264,7 +278,8 @@ __global__ __launch_bounds__(256) void gcm_blocks(GcmBatch a, uint32_t wgs_per_s
             // Horner step with H^64
             if (j) {
                 uint32_t m[4];
-                gf_mul(m, acc, L.htab[63], L.rem);
+                if (UPLINK_GCM_EXP != 1) gf_mul(m, acc, L.htab[63], L.rem);
+                else m[0] = acc[0], m[1] = acc[1], m[2] = acc[2], m[3] = acc[3];
 #pragma unroll
                 for (int q = 0; q < 4; q++) acc[q] = m[q] ^ y[q];
             } else {
