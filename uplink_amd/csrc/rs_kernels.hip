@@ -47,12 +47,13 @@ __constant__ GfTables d_gf = make_gf_tables();
 // them and fill the other slot of a 2-slot LDS ring.  One LDS-only barrier
 // per item, so loads of item i+1 and the stores of item i overlap the XOR
 // work of item i and nothing waits for store completion.
-constexpr int kNC = 4;  // compute waves
-constexpr int kNL = 4;  // loader waves
-constexpr int kThreads = (kNC + kNL) * 64;
-
-template <int K, int N>
-__global__ __launch_bounds__(kThreads, 1) void rs_encode_special(const RsArgs a) {
+// NC compute waves, NL loader waves.  4 + 4 for the full encode (memory-bound:
+// the loaders also write the k data pieces); 8 + 4 for the parity-only
+// encode, where the loaders have less to do and one compute wave per SIMD,
+// issuing at half rate on its own, would be the limit.
+template <int K, int N, int NC, int NL>
+__global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
+    constexpr int kNC = NC, kNL = NL;
     constexpr int R = N - K;
     constexpr int OPW = (R + kNC - 1) / kNC;
     constexpr int PER = (K + kNL - 1) / kNL;
@@ -236,7 +237,15 @@ hipError_t launch_special(const RsArgs &a, int grid, hipStream_t s) {
     // LDS ring = 2 * K * 2 KiB; one workgroup per CU for K = 29, two for small K
     const int per_cu = (2 * K * 2048) * 2 <= 160 * 1024 ? 2 : 1;
     if (grid <= 0) grid = default_grid(a.total_tiles, per_cu);
-    hipLaunchKernelGGL((rs_encode_special<K, N>), dim3(grid), dim3(kThreads), 0, s, a);
+    const bool parity_only = a.copy_off[0] < 0;
+#ifndef UPLINK_ENC_PO_NC
+#define UPLINK_ENC_PO_NC 8
+#endif
+    constexpr int PNC = UPLINK_ENC_PO_NC;
+    if (parity_only && N - K >= PNC * 4)
+        hipLaunchKernelGGL((rs_encode_special<K, N, PNC, 4>), dim3(grid), dim3((PNC + 4) * 64), 0, s, a);
+    else
+        hipLaunchKernelGGL((rs_encode_special<K, N, 4, 4>), dim3(grid), dim3(8 * 64), 0, s, a);
     return hipGetLastError();
 }
 }  // namespace
