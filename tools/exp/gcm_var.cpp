@@ -61,8 +61,8 @@ int main() {
     CK(hipMemcpy(r.data(), back, pbytes, hipMemcpyDeviceToHost));
     uint64_t sum = 0;
     for (size_t i = 0; i < cbytes; i += 7) sum = sum * 1099511628211ull + c[i];
-    printf("tables %d copies %2d exp %d: seal %7.1f us/seg (%5.0f GB/s)  open %7.1f us/seg (%5.0f GB/s)  round trip %s  sum %016llx\n",
-           UPLINK_GCM_TABLES, UPLINK_GCM_COPIES, UPLINK_GCM_EXP, ms[0] * 1e3 / NSEG, pbytes / (ms[0] * 1e6), ms[1] * 1e3 / NSEG, pbytes / (ms[1] * 1e6),
+    printf("lin %d tables %d copies %2d exp %d: seal %7.1f us/seg (%5.0f GB/s)  open %7.1f us/seg (%5.0f GB/s)  round trip %s  sum %016llx\n",
+           UPLINK_GCM_LIN, UPLINK_GCM_TABLES, UPLINK_GCM_COPIES, UPLINK_GCM_EXP, ms[0] * 1e3 / NSEG, pbytes / (ms[0] * 1e6), ms[1] * 1e3 / NSEG, pbytes / (ms[1] * 1e6),
            r == h ? "ok" : "BAD", (unsigned long long)sum);
     return 0;
 }

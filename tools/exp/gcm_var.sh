@@ -4,11 +4,12 @@ D=$(dirname "$0")
 # variants: copies (T-table layout) and exp (1 = no GHASH multiplies, 2 = no AES)
 V=${V:-"0:0 32:0 64:0 32:1 32:2"}
 TB=${TB:-1}
+LIN=${LIN:-1}
 if [ "$1" = run ]; then
-  for v in $V; do timeout -k 5 60 $D/gcm_var_${v/:/_}_t$TB || exit 1; done
+  for v in $V; do timeout -k 5 60 $D/gcm_var_${v/:/_}_t${TB}_l$LIN || exit 1; done
 else
   for v in $V; do
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -x hip -DUPLINK_GCM_COPIES=${v%:*} -DUPLINK_GCM_EXP=${v#*:} -DUPLINK_GCM_TABLES=$TB \
-      $D/gcm_var.cpp -o $D/gcm_var_${v/:/_}_t$TB || exit 1
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -x hip -DUPLINK_GCM_COPIES=${v%:*} -DUPLINK_GCM_EXP=${v#*:} -DUPLINK_GCM_TABLES=$TB -DUPLINK_GCM_LIN=$LIN \
+      $D/gcm_var.cpp -o $D/gcm_var_${v/:/_}_t${TB}_l$LIN || exit 1
   done
 fi
