@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <vector>
 
 #include "aesgcm.hpp"
 
@@ -512,16 +513,14 @@ size_t ec_gcm_key_bytes(void) { return sizeof(GcmSched); }
 int ec_gcm_prepare_keys(const uint8_t *keys, size_t nkeys, void *dev_keys, ec_stream stream) {
     if (nkeys == 0) return EC_OK;
     if (!keys || !dev_keys) return EC_ERR_INVALID_ARG;
-    GcmSched *host = nullptr;
-    if (hipHostMalloc(reinterpret_cast<void **>(&host), nkeys * sizeof(GcmSched), hipHostMallocDefault) != hipSuccess)
-        return EC_ERR_DEVICE;
-    for (size_t i = 0; i < nkeys; i++) gcm_prepare(keys + 32 * i, host + i);
+    // pageable staging (a pinned allocation per call costs more than the 16 KB copy)
+    std::vector<GcmSched> host(nkeys);
+    for (size_t i = 0; i < nkeys; i++) gcm_prepare(keys + 32 * i, &host[i]);
     hipStream_t st = (hipStream_t)stream;
-    int rc = hipMemcpyAsync(dev_keys, host, nkeys * sizeof(GcmSched), hipMemcpyHostToDevice, st) == hipSuccess
+    int rc = hipMemcpyAsync(dev_keys, host.data(), nkeys * sizeof(GcmSched), hipMemcpyHostToDevice, st) == hipSuccess
                  ? EC_OK
                  : EC_ERR_DEVICE;
     if (hipStreamSynchronize(st) != hipSuccess) rc = EC_ERR_DEVICE;  // before the staging buffer goes
-    (void)hipHostFree(host);
     return rc;
 }
 
