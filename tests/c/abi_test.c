@@ -3,7 +3,8 @@
  * no Python or torch in the process.  Checks every ErasureScheme export and
  * the host-memory batch pipeline against the CPU oracle (test
  * infrastructure: oracle/infectious_oracle.c), plus the pinned error codes
- * and strings.  Built by `make -C tests/c`, run by tests/test_c_abi.py on a
+ * and strings, and the BLAKE3 / AES-256-GCM entry points against
+ * oracle/blake3_oracle.c and oracle/aesgcm_oracle.c.  Built by `make -C tests/c`, run by tests/test_c_abi.py on a
  * GPU box.  Exit status 0 = all checks passed. */
 #include <stdint.h>
 #include <stdio.h>
@@ -18,6 +19,11 @@ int or_encode(int k, int n, const uint8_t *enc, const uint8_t *in, size_t in_len
 int or_decode(int k, int n, const uint8_t *enc, int ns, int *numbers, uint8_t **data, size_t len, uint8_t *out);
 int or_baseline_encode_segment(int k, int n, int ess, const uint8_t *enc, const uint8_t *seg, size_t stripes,
                                uint8_t *pieces, int threads);
+
+/* oracles of the adjacent stages */
+void b3_hash(const uint8_t *in, size_t len, uint8_t out[32]);
+int64_t ag_encrypt_blocks(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *plain, size_t nblocks,
+                          size_t in_block, uint8_t *out, int threads);
 
 static int failures = 0;
 #define CHECK(cond, ...)                                                                                \
@@ -142,6 +148,40 @@ static void scheme_surface(int k, int n, int ess) {
     ec_destroy(ctx);
 }
 
+/* BLAKE3 piece hashes and AES-256-GCM blocks through the host entry points */
+static void adjacent_stages(void) {
+    const size_t lens[] = {0, 1, 1024, 1025, 300000};
+    for (size_t t = 0; t < sizeof lens / sizeof lens[0]; t++) {
+        const size_t len = lens[t], np = 3;
+        uint8_t *buf = malloc(np * len + 1), h[3 * 32], want[32];
+        fill(buf, np * len + 1);
+        CHECK(ec_blake3_host(buf, np, (long long)len, len, h) == EC_OK, "ec_blake3_host len %zu", len);
+        for (size_t j = 0; j < np; j++) {
+            b3_hash(buf + j * len, len, want);
+            CHECK(memcmp(h + 32 * j, want, 32) == 0, "BLAKE3 piece %zu of length %zu", j, len);
+        }
+        free(buf);
+    }
+    uint8_t key[32], nonce[12];
+    fill(key, 32);
+    fill(nonce, 12);
+    nonce[0] = 0xfe; /* the block counter carries into byte 1 */
+    const size_t nb = 40, ib = 7408, ob = ib + 16;
+    uint8_t *plain = malloc(nb * ib), *ct = malloc(nb * ob), *ref = malloc(nb * ob), *back = malloc(nb * ib);
+    fill(plain, nb * ib);
+    CHECK(ec_gcm_seal_host(key, nonce, plain, nb, ib, ct) == EC_OK, "ec_gcm_seal_host");
+    CHECK(ag_encrypt_blocks(key, nonce, plain, nb, ib, ref, 4) == -1, "oracle seal");
+    CHECK(memcmp(ct, ref, nb * ob) == 0, "GCM ciphertext || tag != oracle");
+    long long bad = 0;
+    CHECK(ec_gcm_open_host(key, nonce, ct, nb, ib, back, &bad) == EC_OK && bad == -1, "ec_gcm_open_host");
+    CHECK(memcmp(back, plain, nb * ib) == 0, "GCM round trip");
+    ct[17 * ob + ib + 3] ^= 1; /* a tag byte of block 17 */
+    int rc = ec_gcm_open_host(key, nonce, ct, nb, ib, back, &bad);
+    CHECK(rc == EC_ERR_AUTH && bad == 17, "tampered tag -> rc %d block %lld", rc, bad);
+    CHECK(strcmp(ec_strerror(EC_ERR_AUTH), "cipher: message authentication failed") == 0, "auth error text");
+    free(plain), free(ct), free(ref), free(back);
+}
+
 int main(void) {
     ec_ctx *bad = NULL;
     CHECK(ec_create(0, 4, 256, &bad) == EC_ERR_PARAMS, "k = 0");
@@ -149,6 +189,7 @@ int main(void) {
     CHECK(ec_device_count() >= 1, "no device");
     const int cfg[][3] = {{2, 4, 1024}, {4, 10, 256}, {29, 80, 256}, {20, 60, 4096}, {3, 7, 100}, {10, 20, 64}};
     for (size_t i = 0; i < sizeof cfg / sizeof cfg[0]; i++) scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2]);
+    adjacent_stages();
     printf("%s: %d failures\n", failures ? "FAIL" : "ok", failures);
     return failures ? 1 : 0;
 }

@@ -11,7 +11,6 @@ from oracle import aesgcm as oa
 from oracle import blake3 as ob
 from oracle import oracle as O
 
-pytestmark = pytest.mark.gpu
 
 
 def _torch():
@@ -24,11 +23,20 @@ def _torch():
 def test_geometry_matches_reference_sizes():
     """64 MiB plaintext: 9059 GCM blocks = 67,254,016 B = 9059 stripes, padded
     to 9060 stripes (2,319,360-byte pieces), SURVEY Appendix B."""
-    from uplink_amd import eestream, pipeline
-    g = pipeline.SegmentGeometry(64 * 2**20, eestream.RSScheme(eestream.new_fec(29, 80), 256))
+    from uplink_amd import pipeline
+
+    class Sizes:  # the two sizes SegmentGeometry reads from an RSScheme (no device needed)
+        def stripe_size(self):
+            return 29 * 256
+
+        def erasure_share_size(self):
+            return 256
+
+    g = pipeline.SegmentGeometry(64 * 2**20, Sizes())
     assert (g.nblocks, g.enc_len, g.nstripes, g.piece_len) == (9059, 67254016, 9060, 2319360)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("k,n,plain_len,nseg", [(29, 80, 64 * 2**20, 2), (29, 80, 100_000, 3), (4, 10, 7407, 2),
                                                 (29, 80, 1, 1)])
 def test_upload_download_chain(k, n, plain_len, nseg):
