@@ -357,16 +357,20 @@ const char *ec_encode_kernel_name(const ec_ctx *c) {
     return have_special_encoder(c->k, c->n) ? "special" : "generic";
 }
 
-int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
-                       int flags, ec_stream stream) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
+// Encode stripes [s0, s1) of nseg segments of nstripes stripes each: the
+// pieces keep their full layout ([seg][rows][nstripes*ess]), the range
+// writes its part of every piece (used to pipeline one segment through PCIe
+// in chunks of stripes).
+static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, size_t s0, size_t s1,
+                        uint8_t *pieces, int flags, hipStream_t s) {
     if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
-    if (nseg == 0 || nstripes == 0) return EC_OK;
+    if (nseg == 0 || s1 <= s0) return EC_OK;
     const int k = c->k, n = c->n, ess = c->ess;
     if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
-    hipStream_t s = (hipStream_t)stream;
     const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
     const int64_t piece_len = (int64_t)nstripes * ess;
+    segs += s0 * (size_t)k * ess;
+    pieces += s0 * (size_t)ess;
     RsArgs a{};
     a.in_base = segs;
     a.out_base = pieces;
@@ -385,7 +389,7 @@ int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_
     int64_t out_off[256];
     for (int r = 0; r < n - k; r++) out_off[r] = (int64_t)(parity_only ? r : k + r) * piece_len;
     for (int r = 0; r < std::min(n - k, kMaxOps); r++) a.out_off[r] = out_off[r];
-    fill_geometry(a, ess, (int64_t)nstripes, (int64_t)nseg);
+    fill_geometry(a, ess, (int64_t)(s1 - s0), (int64_t)nseg);
     const bool bits = (ess % 16) == 0 && aligned16(segs) && aligned16(pieces);
     if (bits && have_special_encoder(k, n)) {
         HIP_TRY(launch_encode_special(k, n, a, 0, s));
@@ -413,6 +417,12 @@ int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_
         return EC_OK;
     }
     return run_matmul(a, (int64_t)nseg, bits, s);
+}
+
+int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                       int flags, ec_stream stream) {
+    return encode_range(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, 0, nstripes, pieces, flags,
+                        (hipStream_t)stream);
 }
 
 int ec_rebuild_segments_batched(const ec_ctx *cc, int nshares, const int *nums, const uint8_t *const *pieces,
@@ -640,44 +650,75 @@ static int hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *pa
     return EC_OK;
 }
 
+// Host pipeline of the encode.  The three pipe streams take roles (H2D,
+// compute, D2H) and every segment goes through in chunks of stripes, so the
+// upload of chunk i+1, the encode of chunk i and the download of chunk i-1
+// overlap, and PCIe carries both directions at once (it is full duplex:
+// ~57 GB/s each way, ~97 GB/s both, tools/exp/pcie_probe.py).  Segments
+// rotate over the three device slots; a slot is reused once its D2H is done.
 static int encode_host(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
                        uint8_t *hashes, int flags) {
     if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
     if (nseg == 0 || nstripes == 0) return EC_OK;
-    const size_t spad = nstripes * (size_t)c->k * c->ess;
+    const size_t ess = c->ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
     const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
     const int rows = parity_only ? c->n - c->k : c->n;
-    const size_t pbytes = (size_t)rows * nstripes * c->ess;
+    const size_t plen = nstripes * ess, pbytes = (size_t)rows * plen;
     // device slot: pieces | hashes (n*32) | BLAKE3 workspace
     const size_t hash_at = align_up(pbytes, 256), ws_at = hash_at + align_up(32 * (size_t)c->n, 256);
-    const size_t out_cap = hashes ? ws_at + b3_segment_ws_bytes(c, 1, nstripes) : pbytes;
+    const size_t out_cap = hashes ? ws_at + b3_segment_ws_bytes(c, 1, nstripes) : std::max<size_t>(pbytes, 1);
+    const size_t nch = std::min<size_t>(8, std::max<size_t>(1, nstripes / 256));
+    const size_t chunk = (nstripes + nch - 1) / nch;
     std::lock_guard<std::mutex> g(c->pipe_mu);
     int rc = pipe_reserve(c, spad, out_cap);
     if (rc) return rc;
-    for (size_t s = 0; s < nseg && rc == EC_OK; s++) {
-        const int slot = (int)(s % HostPipe::kSlots);
-        hipStream_t st = c->pipe.st[slot];
-        uint8_t *d_out = c->pipe.d_out[slot];
-        if (hipMemcpyAsync(c->pipe.d_in[slot], segs + s * spad, spad, hipMemcpyHostToDevice, st) != hipSuccess) {
+    hipStream_t h2d = c->pipe.st[0], comp = c->pipe.st[1], d2h = c->pipe.st[2];
+    std::vector<hipEvent_t> ev(2 * nch + 1 + HostPipe::kSlots, nullptr);
+    for (auto &e : ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = EC_ERR_DEVICE;
+    hipEvent_t *ev_in = ev.data(), *ev_enc = ev.data() + nch, ev_hash = ev[2 * nch];
+    hipEvent_t *slot_free = ev.data() + 2 * nch + 1;
+    for (size_t sg = 0; sg < nseg && rc == EC_OK; sg++) {
+        const int slot = (int)(sg % HostPipe::kSlots);
+        uint8_t *d_in = c->pipe.d_in[slot], *d_out = c->pipe.d_out[slot];
+        if (sg >= (size_t)HostPipe::kSlots && hipStreamWaitEvent(h2d, slot_free[slot], 0) != hipSuccess) {
             rc = EC_ERR_DEVICE;
             break;
         }
-        if (rows > 0) rc = ec_encode_segments(c, c->pipe.d_in[slot], 1, nstripes, d_out, flags, st);
-        if (rc) break;
-        if (hashes) {
-            const uint8_t *parity = d_out + (parity_only ? 0 : (size_t)c->k * nstripes * c->ess);
-            rc = hash_segments(c, c->pipe.d_in[slot], parity, 1, nstripes, d_out + hash_at, d_out + ws_at, st);
-            if (rc) break;
-            if (hipMemcpyAsync(hashes + s * 32 * (size_t)c->n, d_out + hash_at, 32 * (size_t)c->n,
-                               hipMemcpyDeviceToHost, st) != hipSuccess) {
+        for (size_t ch = 0; ch < nch && rc == EC_OK; ch++) {
+            const size_t s0 = ch * chunk, s1 = std::min(nstripes, s0 + chunk);
+            if (s0 >= s1) break;
+            if (hipMemcpyAsync(d_in + s0 * stripe, segs + sg * spad + s0 * stripe, (s1 - s0) * stripe,
+                               hipMemcpyHostToDevice, h2d) != hipSuccess ||
+                hipEventRecord(ev_in[ch], h2d) != hipSuccess || hipStreamWaitEvent(comp, ev_in[ch], 0) != hipSuccess) {
                 rc = EC_ERR_DEVICE;
                 break;
             }
+            if (rows > 0) rc = encode_range(c, d_in, 1, nstripes, s0, s1, d_out, flags, comp);
+            if (rc) break;
+            if (hipEventRecord(ev_enc[ch], comp) != hipSuccess || hipStreamWaitEvent(d2h, ev_enc[ch], 0) != hipSuccess) {
+                rc = EC_ERR_DEVICE;
+                break;
+            }
+            if (rows > 0 && hipMemcpy2DAsync(pieces + sg * pbytes + s0 * ess, plen, d_out + s0 * ess, plen,
+                                             (s1 - s0) * ess, rows, hipMemcpyDeviceToHost, d2h) != hipSuccess)
+                rc = EC_ERR_DEVICE;
         }
-        if (pbytes && hipMemcpyAsync(pieces + s * pbytes, d_out, pbytes, hipMemcpyDeviceToHost, st) != hipSuccess)
-            rc = EC_ERR_DEVICE;
+        if (rc == EC_OK && hashes) {
+            const uint8_t *parity = d_out + (parity_only ? 0 : (size_t)c->k * plen);
+            rc = hash_segments(c, d_in, parity, 1, nstripes, d_out + hash_at, d_out + ws_at, comp);
+            if (rc == EC_OK &&
+                (hipEventRecord(ev_hash, comp) != hipSuccess || hipStreamWaitEvent(d2h, ev_hash, 0) != hipSuccess ||
+                 hipMemcpyAsync(hashes + sg * 32 * (size_t)c->n, d_out + hash_at, 32 * (size_t)c->n,
+                                hipMemcpyDeviceToHost, d2h) != hipSuccess))
+                rc = EC_ERR_DEVICE;
+        }
+        if (rc == EC_OK && hipEventRecord(slot_free[slot], d2h) != hipSuccess) rc = EC_ERR_DEVICE;
     }
-    return pipe_drain(c, rc);
+    rc = pipe_drain(c, rc);
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return rc;
 }
 
 int ec_encode_segments_host(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
@@ -749,33 +790,56 @@ int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, con
     std::vector<int> order, ids;
     int rc = choose_shares(c, nshares, nums, order, ids);
     if (rc) return rc;
-    const size_t plen = nstripes * c->ess;
-    const size_t spad = nstripes * (size_t)c->k * c->ess;
+    const size_t ess = c->ess, plen = nstripes * ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
+    // chunks of stripes through the role streams, as encode_host
+    const size_t nch = std::min<size_t>(8, std::max<size_t>(1, nstripes / 256));
+    const size_t chunk = (nstripes + nch - 1) / nch;
     std::lock_guard<std::mutex> g(c->pipe_mu);
     rc = pipe_reserve(c, plen * c->k, spad);
     if (rc) return rc;
+    hipStream_t h2d = c->pipe.st[0], comp = c->pipe.st[1], d2h = c->pipe.st[2];
+    std::vector<hipEvent_t> ev(2 * nch + HostPipe::kSlots, nullptr);
+    for (auto &e : ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = EC_ERR_DEVICE;
+    hipEvent_t *ev_in = ev.data(), *ev_out = ev.data() + nch, *slot_free = ev.data() + 2 * nch;
     std::vector<int> knums(c->k);
-    for (size_t s = 0; s < nseg && rc == EC_OK; s++) {
-        const int slot = (int)(s % HostPipe::kSlots);
-        hipStream_t st = c->pipe.st[slot];
-        std::vector<const uint8_t *> dptr(c->k);
-        for (int i = 0; i < c->k; i++) {
-            const uint8_t *src = pieces[order[i]] + (int64_t)s * piece_seg_stride;
-            if (hipMemcpyAsync(c->pipe.d_in[slot] + plen * i, src, plen, hipMemcpyHostToDevice, st) != hipSuccess) {
-                rc = EC_ERR_DEVICE;
+    for (int i = 0; i < c->k; i++) knums[i] = ids[i];
+    std::vector<const uint8_t *> dptr(c->k);
+    for (size_t sg = 0; sg < nseg && rc == EC_OK; sg++) {
+        const int slot = (int)(sg % HostPipe::kSlots);
+        uint8_t *d_in = c->pipe.d_in[slot], *d_out = c->pipe.d_out[slot];
+        if (sg >= (size_t)HostPipe::kSlots && hipStreamWaitEvent(h2d, slot_free[slot], 0) != hipSuccess) {
+            rc = EC_ERR_DEVICE;
+            break;
+        }
+        for (size_t ch = 0; ch < nch && rc == EC_OK; ch++) {
+            const size_t s0 = ch * chunk, s1 = std::min(nstripes, s0 + chunk);
+            if (s0 >= s1) break;
+            for (int i = 0; i < c->k && rc == EC_OK; i++) {
+                const uint8_t *src = pieces[order[i]] + (int64_t)sg * piece_seg_stride + s0 * ess;
+                if (hipMemcpyAsync(d_in + plen * i + s0 * ess, src, (s1 - s0) * ess, hipMemcpyHostToDevice, h2d) !=
+                    hipSuccess)
+                    rc = EC_ERR_DEVICE;
+                dptr[i] = d_in + plen * i + s0 * ess;
+            }
+            if (rc || hipEventRecord(ev_in[ch], h2d) != hipSuccess || hipStreamWaitEvent(comp, ev_in[ch], 0) != hipSuccess) {
+                rc = rc ? rc : EC_ERR_DEVICE;
                 break;
             }
-            dptr[i] = c->pipe.d_in[slot] + plen * i;
-            knums[i] = ids[i];
+            rc = rebuild_device(c, c->k, knums.data(), dptr.data(), c->ess, (int64_t)(s1 - s0), 1, 0, 0,
+                                d_out + s0 * stripe, comp);
+            if (rc) break;
+            if (hipEventRecord(ev_out[ch], comp) != hipSuccess || hipStreamWaitEvent(d2h, ev_out[ch], 0) != hipSuccess ||
+                hipMemcpyAsync(out + sg * spad + s0 * stripe, d_out + s0 * stripe, (s1 - s0) * stripe,
+                               hipMemcpyDeviceToHost, d2h) != hipSuccess)
+                rc = EC_ERR_DEVICE;
         }
-        if (rc) break;
-        rc = rebuild_device(c, c->k, knums.data(), dptr.data(), c->ess, (int64_t)nstripes, 1, 0, 0,
-                            c->pipe.d_out[slot], st);
-        if (rc) break;
-        if (hipMemcpyAsync(out + s * spad, c->pipe.d_out[slot], spad, hipMemcpyDeviceToHost, st) != hipSuccess)
-            rc = EC_ERR_DEVICE;
+        if (rc == EC_OK && hipEventRecord(slot_free[slot], d2h) != hipSuccess) rc = EC_ERR_DEVICE;
     }
-    return pipe_drain(c, rc);
+    rc = pipe_drain(c, rc);
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return rc;
 }
 
 int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out) {
