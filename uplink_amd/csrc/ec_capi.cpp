@@ -791,8 +791,18 @@ int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, con
     int rc = choose_shares(c, nshares, nums, order, ids);
     if (rc) return rc;
     const size_t ess = c->ess, plen = nstripes * ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
-    // chunks of stripes through the role streams, as encode_host
-    const size_t nch = std::min<size_t>(8, std::max<size_t>(1, nstripes / 256));
+    // The k chosen pieces usually sit at one stride in host memory (one buffer per segment): then
+    // each chunk is one 2D copy.  Otherwise every piece is its own copy per chunk, and chunks are
+    // kept >= 1 MiB per piece so the per-copy cost stays small.
+    int64_t pstride = 0;
+    bool strided = c->k > 1;
+    if (strided) {
+        pstride = pieces[order[1]] - pieces[order[0]];
+        for (int i = 2; i < c->k && strided; i++) strided = pieces[order[i]] - pieces[order[i - 1]] == pstride;
+        strided = strided && pstride >= (int64_t)plen;
+    }
+    const size_t nch = strided ? std::min<size_t>(8, std::max<size_t>(1, nstripes / 256))
+                               : std::min<size_t>(8, std::max<size_t>(1, plen >> 20));
     const size_t chunk = (nstripes + nch - 1) / nch;
     std::lock_guard<std::mutex> g(c->pipe_mu);
     rc = pipe_reserve(c, plen * c->k, spad);
@@ -815,12 +825,18 @@ int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, con
         for (size_t ch = 0; ch < nch && rc == EC_OK; ch++) {
             const size_t s0 = ch * chunk, s1 = std::min(nstripes, s0 + chunk);
             if (s0 >= s1) break;
-            for (int i = 0; i < c->k && rc == EC_OK; i++) {
-                const uint8_t *src = pieces[order[i]] + (int64_t)sg * piece_seg_stride + s0 * ess;
-                if (hipMemcpyAsync(d_in + plen * i + s0 * ess, src, (s1 - s0) * ess, hipMemcpyHostToDevice, h2d) !=
-                    hipSuccess)
+            for (int i = 0; i < c->k; i++) dptr[i] = d_in + plen * i + s0 * ess;
+            if (strided) {
+                if (hipMemcpy2DAsync(d_in + s0 * ess, plen, pieces[order[0]] + (int64_t)sg * piece_seg_stride + s0 * ess,
+                                     (size_t)pstride, (s1 - s0) * ess, c->k, hipMemcpyHostToDevice, h2d) != hipSuccess)
                     rc = EC_ERR_DEVICE;
-                dptr[i] = d_in + plen * i + s0 * ess;
+            } else {
+                for (int i = 0; i < c->k && rc == EC_OK; i++) {
+                    const uint8_t *src = pieces[order[i]] + (int64_t)sg * piece_seg_stride + s0 * ess;
+                    if (hipMemcpyAsync(d_in + plen * i + s0 * ess, src, (s1 - s0) * ess, hipMemcpyHostToDevice, h2d) !=
+                        hipSuccess)
+                        rc = EC_ERR_DEVICE;
+                }
             }
             if (rc || hipEventRecord(ev_in[ch], h2d) != hipSuccess || hipStreamWaitEvent(comp, ev_in[ch], 0) != hipSuccess) {
                 rc = rc ? rc : EC_ERR_DEVICE;
