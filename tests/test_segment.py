@@ -71,3 +71,41 @@ def test_piece_reader_num_errors():
         spr.piece_reader(-1)
     with pytest.raises(eestream.InfectiousError, match="num must be less than 10"):
         spr.piece_reader(10)
+
+
+@pytest.mark.parametrize("k,n,ess,stripes,nseg", [(29, 80, 256, 1000, 5), (20, 60, 4096, 300, 4), (4, 10, 256, 257, 7),
+                                                  (29, 80, 256, 9040, 2)])
+def test_chunked_host_pipelines(oracle, k, n, ess, stripes, nseg):
+    """ec_encode_segments_host / ec_rebuild_segments_host move each segment in
+    chunks of stripes over three role streams and rotate segments over three
+    device slots: ragged last chunks, more segments than slots, both output
+    layouts, and rebuild inputs both in one strided buffer (one 2D copy per
+    chunk) and at scattered pointers (one copy per piece)."""
+    import ctypes
+    from uplink_amd import _native as N
+    lib = N.load()
+    sch = eestream.RSScheme(eestream.new_fec(k, n), ess)
+    plen, spad = stripes * ess, stripes * k * ess
+    rng = np.random.default_rng(stripes + nseg)
+    segs = rng.integers(0, 256, (nseg, spad), dtype=np.uint8)
+    fec = oracle.FEC(k, n)
+    ref = np.stack([fec.encode_segment(segs[g], ess, threads=8) for g in range(nseg)])
+    for flags, rows in ((0, n), (N.EC_FLAG_PARITY_ONLY, n - k)):
+        pieces = np.zeros((nseg, rows, plen), dtype=np.uint8)
+        assert lib.ec_encode_segments_host(sch.ctx, segs.ctypes.data, nseg, stripes, pieces.ctypes.data, flags) == 0
+        assert np.array_equal(pieces, ref[:, n - rows:]), flags
+    full = np.ascontiguousarray(ref)
+    nums = sorted(rng.choice(n, k, replace=False).tolist())
+    # strided: the chosen pieces inside one [nseg][n][plen] buffer
+    out = np.zeros((nseg, spad), dtype=np.uint8)
+    c_nums = (ctypes.c_int * k)(*nums)
+    c_ptrs = (ctypes.c_void_p * k)(*[full.ctypes.data + i * plen for i in nums])
+    assert lib.ec_rebuild_segments_host(sch.ctx, k, c_nums, c_ptrs, stripes, nseg, n * plen, out.ctypes.data) == 0
+    assert np.array_equal(out, segs)
+    # scattered: every chosen piece of every segment in its own buffer, at one segment stride
+    scat = [np.ascontiguousarray(full[:, i, :]) for i in nums]  # [nseg][plen] each
+    c_ptrs2 = (ctypes.c_void_p * k)(*[a.ctypes.data for a in scat[::-1]])
+    c_nums2 = (ctypes.c_int * k)(*nums[::-1])
+    out2 = np.zeros((nseg, spad), dtype=np.uint8)
+    assert lib.ec_rebuild_segments_host(sch.ctx, k, c_nums2, c_ptrs2, stripes, nseg, plen, out2.ctypes.data) == 0
+    assert np.array_equal(out2, segs)
