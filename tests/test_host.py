@@ -107,3 +107,22 @@ def test_no_cpu_fallback_without_gpu(native):
     assert native.ec_create(29, 80, 256, ctypes.byref(h)) == _native.EC_ERR_DEVICE
     with pytest.raises(eestream.DeviceError):
         eestream.RSScheme(eestream.new_fec(29, 80), 256)
+
+
+def test_adjacent_stage_entry_points_validate_before_the_device(native):
+    """The BLAKE3 / AES-GCM / padding exports reject bad arguments (and accept
+    empty work) without touching a device, like the RS exports."""
+    assert native.ec_gcm_key_bytes() >= 60 * 4 + 64 * 16 * 16
+    assert native.ec_blake3_pieces(None, 0, 0, 0, 0, 0, None, None) == _native.EC_ERR_INVALID_ARG  # no output
+    out = ctypes.create_string_buffer(32)
+    assert native.ec_blake3_pieces(None, 0, 0, 0, 0, 0, out, None) == _native.EC_OK  # nothing to hash
+    assert native.ec_blake3_pieces(None, 1, 0, 10, 0, 0, out, None) == _native.EC_ERR_INVALID_ARG
+    assert native.ec_gcm_prepare_keys(None, 0, None, None) == _native.EC_OK
+    assert native.ec_gcm_prepare_keys(None, 1, None, None) == _native.EC_ERR_INVALID_ARG
+    assert native.ec_gcm_seal_segments(None, 1, 1, 7408, None, None, None, None) == _native.EC_ERR_INVALID_ARG
+    assert native.ec_gcm_seal_segments(None, 0, 1, 7408, None, None, None, None) == _native.EC_OK
+    assert native.ec_gcm_open_segments(None, 1, 1, 7408, None, None, None, None, None) == _native.EC_ERR_INVALID_ARG
+    assert native.ec_gcm_seal_host(None, None, None, 0, 7408, None) == _native.EC_ERR_INVALID_ARG
+    assert native.ec_pad_segments(None, 1, 0, 10, 16, None) == _native.EC_ERR_INVALID_ARG
+    assert native.ec_pad_segments(None, 0, 0, 10, 16, None) == _native.EC_OK
+    assert native.ec_strerror(_native.EC_ERR_AUTH).decode() == "cipher: message authentication failed"
