@@ -102,56 +102,88 @@ struct B3Pair {
     uint64_t split;
 };
 
+// chunks per lane.  2 folds the first tree level in registers at full lane
+// utilisation (the LDS fold then starts from 256 level-1 nodes), but halves
+// the waves in flight: 72.5 against 67.9 us per segment, so 1.
+#ifndef UPLINK_B3_PAIR
+#define UPLINK_B3_PAIR 1
+#endif
+constexpr int kPerLane = UPLINK_B3_PAIR;
+constexpr int kGroupChunks = kGroup * kPerLane;  // chunks per workgroup
+
+// CV of chunk c of a piece (ROOT on its last block when `root`)
+template <bool kFast>
+__device__ __forceinline__ void chunk_cv(const B3View &v, const uint8_t *pb, uint64_t c, bool root, uint32_t (&h)[8]) {
+    const uint64_t t0 = c * 1024;
+    const uint64_t clen = v.piece_len - t0 < 1024 ? v.piece_len - t0 : 1024;  // 0 only for an empty piece
+#pragma unroll
+    for (int i = 0; i < 8; i++) h[i] = kIV[i];
+    if (UPLINK_B3_LINES && kFast && clen == 1024 && v.run_shift >= 7) {
+        full_chunk_lines(v, pb, t0, c, kChunkEnd | (root ? kRoot : 0), h);
+        return;
+    }
+    // partial chunk, 64-byte runs, or the byte path: block by block
+    const uint32_t nb = clen ? (uint32_t)((clen + 63) >> 6) : 1;
+    uint32_t m[16], nx[16];
+    load_block<kFast>(v, pb, t0, nb == 1 ? (uint32_t)clen : 64, m);
+    for (uint32_t b = 0; b < nb; b++) {
+        const bool last = b + 1 == nb;
+        const uint32_t blen = last ? (uint32_t)(clen - 64ull * b) : 64;
+        if (!last) {  // prefetch the next block while this one compresses
+            const uint32_t nlen = b + 2 == nb ? (uint32_t)(clen - 64ull * (b + 1)) : 64;
+            load_block<kFast>(v, pb, t0 + 64ull * (b + 1), nlen, nx);
+        }
+        const uint32_t flags = (b == 0 ? kChunkStart : 0) | (last ? kChunkEnd : 0) | (last && root ? kRoot : 0);
+        compress(h, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
+        if (!last) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) m[i] = nx[i];
+        }
+    }
+}
+
 template <bool kFast>
 __global__ __launch_bounds__(kGroup) void b3_chunks(B3Pair pv, uint64_t nchunks, uint32_t groups, uint32_t *nodes,
                                                      uint8_t *hashes) {
     __shared__ uint32_t lds[2][8][kGroup];
     const uint64_t piece = blockIdx.x / groups;
     const uint32_t group = blockIdx.x % groups;
-    const uint64_t c = (uint64_t)group * kGroup + threadIdx.x;
-    const bool single = nchunks == 1;
+    const uint64_t c0 = (uint64_t)group * kGroupChunks + (uint64_t)threadIdx.x * kPerLane;
     const bool second = piece >= pv.split;
     const B3View &v = pv.v[second];
     const uint8_t *pb = piece_base(v, second ? piece - pv.split : piece);
-    if (c < nchunks) {
-        const uint64_t t0 = c * 1024;
-        const uint64_t clen = v.piece_len - t0 < 1024 ? v.piece_len - t0 : 1024;  // 0 only for an empty piece
-        uint32_t h[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) h[i] = kIV[i];
-        if (UPLINK_B3_LINES && kFast && clen == 1024 && v.run_shift >= 7) {
-            full_chunk_lines(v, pb, t0, c, kChunkEnd | (single ? kRoot : 0), h);
-        } else {  // partial chunk, 64-byte runs, or the byte path: block by block
-            const uint32_t nb = clen ? (uint32_t)((clen + 63) >> 6) : 1;
-            uint32_t m[16], nx[16];
-            load_block<kFast>(v, pb, t0, nb == 1 ? (uint32_t)clen : 64, m);
-            for (uint32_t b = 0; b < nb; b++) {
-                const bool last = b + 1 == nb;
-                const uint32_t blen = last ? (uint32_t)(clen - 64ull * b) : 64;
-                if (!last) {  // prefetch the next block while this one compresses
-                    const uint32_t nlen = b + 2 == nb ? (uint32_t)(clen - 64ull * (b + 1)) : 64;
-                    load_block<kFast>(v, pb, t0 + 64ull * (b + 1), nlen, nx);
-                }
-                const uint32_t flags =
-                    (b == 0 ? kChunkStart : 0) | (last ? kChunkEnd : 0) | (last && single ? kRoot : 0);
-                compress(h, m, (uint32_t)c, (uint32_t)(c >> 32), blen, flags);
-                if (!last) {
-#pragma unroll
-                    for (int i = 0; i < 16; i++) m[i] = nx[i];
-                }
+    if (nchunks <= (uint64_t)kPerLane) {  // the whole piece is this lane's: it also applies ROOT
+        if (threadIdx.x == 0 && group == 0) {
+            uint32_t h[8];
+            chunk_cv<kFast>(v, pb, 0, nchunks == 1, h);
+            if (nchunks == 2) {
+                uint32_t r[8], p[8];
+                chunk_cv<kFast>(v, pb, 1, false, r);
+                parent(p, h, r, true);
+                store_hash(hashes + 32 * piece, p);
+            } else {
+                store_hash(hashes + 32 * piece, h);
             }
         }
-        if (single) {
-            store_hash(hashes + 32 * piece, h);
-            return;  // the only lane of a one-chunk piece
-        }
+        return;
+    }
+    if (c0 < nchunks) {
+        uint32_t h[8];
+        chunk_cv<kFast>(v, pb, c0, false, h);
+        if (kPerLane == 2 && c0 + 1 < nchunks) {  // the level-1 parent of this lane's pair
+            uint32_t r[8], p[8];
+            chunk_cv<kFast>(v, pb, c0 + 1, false, r);
+            parent(p, h, r, false);
+#pragma unroll
+            for (int i = 0; i < 8; i++) h[i] = p[i];
+        }  // an odd last chunk moves up unchanged
 #pragma unroll
         for (int i = 0; i < 8; i++) lds[0][i][threadIdx.x] = h[i];
     }
-    if (single) return;
     __syncthreads();
-    const uint64_t left = nchunks - (uint64_t)group * kGroup;
-    const int cnt = left < kGroup ? (int)left : kGroup;
+    const uint64_t left = nchunks - (uint64_t)group * kGroupChunks;  // chunks in this group
+    const uint64_t nodes1 = (left < (uint64_t)kGroupChunks ? left : kGroupChunks) + kPerLane - 1;
+    const int cnt = (int)(nodes1 / kPerLane);
     uint32_t h[8];
     fold(lds, cnt, groups == 1, h);
     if (threadIdx.x == 0) {
@@ -201,7 +233,7 @@ uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 size_t b3_workspace_bytes(const B3View &v) {
     // two ping-pong node arrays: level 1 (ceil(chunks/256) per piece) and level 2
-    const uint64_t g1 = ceil_div(chunks_of(v), kGroup);
+    const uint64_t g1 = ceil_div(chunks_of(v), kGroupChunks);
     if (g1 <= 1) return 0;
     const uint64_t g2 = ceil_div(g1, kGroup);
     return (size_t)(v.npieces * (g1 + (g2 > 1 ? g2 : 0)) * 32);
@@ -234,7 +266,7 @@ hipError_t b3_launch2(const B3View &first, const B3View &second, uint8_t *hashes
     for (const B3View &v : pv.v)
         if (v.npieces && !v.base && v.piece_len) return hipErrorInvalidValue;
     const uint64_t nchunks = chunks_of(first.npieces ? first : second);
-    uint64_t groups = ceil_div(nchunks, kGroup);
+    uint64_t groups = ceil_div(nchunks, kGroupChunks);
     if (groups > 0xFFFFFFFFull / kGroup || npieces * groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
     uint32_t *a = static_cast<uint32_t *>(ws);
     uint32_t *b = groups > 1 ? a + npieces * groups * 8 : nullptr;
