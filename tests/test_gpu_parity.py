@@ -437,3 +437,21 @@ def test_unsafe_rs_scheme_decode_is_rebuild(oracle):
     bad[1].data[3] ^= 0x41  # share 2: one of the shares Rebuild takes
     assert not np.array_equal(unsafe.decode(None, [s.deep_copy() for s in bad]), stripe)
     assert np.array_equal(safe.decode(None, bad), stripe)
+
+
+@pytest.mark.parametrize("k,n", [(29, 80), (20, 60), (50, 80)])
+def test_rebuild_every_missing_count(oracle, k, n):
+    """Rebuild with every number m of missing data shares, 0..min(k, n-k):
+    this walks every rebuild kernel width (2, 3 or 4 waves of up to 8 rows,
+    several passes beyond 32 rows), every right-aligned entry point into the
+    call sequence, and the copy-only case m = 0."""
+    ess, stripes = 256, 40
+    sch = scheme(k, n, ess)
+    rng = np.random.default_rng(k * 1000 + n)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    d_pieces = gpu_encode(sch, seg)
+    for m in range(0, min(k, n - k) + 1):
+        data = sorted(rng.choice(k, k - m, replace=False).tolist())
+        parity = sorted(rng.choice(np.arange(k, n), m, replace=False).tolist())
+        nums = data + parity
+        assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), m
