@@ -132,10 +132,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND=gloo rehearses the N > 1 path on a one-GPU box (ranks share the
+    # device, host-side collectives); the driver's multi-GPU runs use the default, RCCL.
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    coll_dev = torch.device("cpu") if backend == "gloo" else None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local if backend != "gloo" else local % torch.cuda.device_count())
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -214,7 +221,7 @@ def main():
         by_set.setdefault(st % len(sets), []).append(ev[st][1].elapsed_time(ev[st][2]) * 1e3 / B)
     if world > 1:
         import torch.distributed as dist
-        tw = torch.tensor([wall], dtype=torch.float64, device=dev)
+        tw = torch.tensor([wall], dtype=torch.float64, device=coll_dev or dev)
         dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         wall = float(tw.item())
 
@@ -238,7 +245,7 @@ def main():
     del par
     if world > 1:
         import torch.distributed as dist
-        v = torch.tensor([1 if verified else 0], device=dev)
+        v = torch.tensor([1 if verified else 0], device=coll_dev or dev)
         dist.all_reduce(v, op=dist.ReduceOp.MIN)
         verified = bool(v.item())
 
