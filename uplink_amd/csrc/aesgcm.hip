@@ -176,8 +176,11 @@ __device__ __forceinline__ void load_tail(const uint8_t *p, uint32_t n, uint32_t
     for (uint32_t i = 0; i < n; i++) w[i >> 2] |= (uint32_t)p[i] << (24 - 8 * (i & 3));
 }
 
+#ifndef UPLINK_GCM_WGS_PER_CU
+#define UPLINK_GCM_WGS_PER_CU 1
+#endif
 template <bool kOpen>
-__global__ __launch_bounds__(256) void gcm_blocks(GcmBatch a, uint32_t wgs_per_seg) {
+__global__ __launch_bounds__(256, UPLINK_GCM_WGS_PER_CU) void gcm_blocks(GcmBatch a, uint32_t wgs_per_seg) {
     __shared__ Lds L;
     const uint32_t seg = blockIdx.x / wgs_per_seg;
     const uint32_t wg = blockIdx.x % wgs_per_seg;
