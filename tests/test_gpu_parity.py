@@ -455,3 +455,37 @@ def test_rebuild_every_missing_count(oracle, k, n):
         parity = sorted(rng.choice(np.arange(k, n), m, replace=False).tolist())
         nums = data + parity
         assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), m
+
+
+@pytest.mark.parametrize("extra,bad,scatter", [(2, 1, 0), (4, 1, 0), (4, 2, 0), (6, 2, 40), (8, 3, 200), (4, 3, 0)])
+def test_decode_bad_pieces_over_long_runs(oracle, extra, bad, scatter):
+    """Decode (Correct + Rebuild) of shares covering many stripes, with whole
+    shares corrupted (bad pieces: every column flagged) plus scattered errors
+    in one other share.  ec_decode locates the bad shares on a sample of
+    columns, rewrites them from the others, and sends only the columns the
+    others disagree on to per-column Berlekamp-Welch; the result must be the
+    codeword, the shares corrected in place, and TooManyErrors beyond e."""
+    k, n, ln = 29, 80, 4096
+    sch = scheme(k, n, 256)
+    rng = np.random.default_rng(extra * 100 + bad * 10 + scatter)
+    data = rng.integers(0, 256, k * ln, dtype=np.uint8)
+    allsh = oracle.FEC(k, n).encode(data)  # [n][ln]: byte column c of every share is one codeword
+    nums = sorted(rng.choice(n, k + extra, replace=False).tolist())
+    recv = [np.array(allsh[i]) for i in nums]
+    bad_idx = [int(i) for i in rng.choice(k + extra, bad, replace=False)]
+    for i in bad_idx:
+        recv[i] ^= rng.integers(1, 256, ln, dtype=np.uint8)
+    if scatter:
+        j = [i for i in range(k + extra) if i not in bad_idx][0]
+        where = rng.choice(ln, scatter, replace=False)
+        recv[j][where] ^= rng.integers(1, 256, scatter, dtype=np.uint8)
+    shares = [eestream.Share(nu, r.copy()) for nu, r in zip(nums, recv)]
+    if bad + (1 if scatter else 0) > extra // 2:
+        with pytest.raises(eestream.InfectiousError):
+            sch.decode(None, shares)
+        return
+    assert np.array_equal(sch.decode(None, shares), data)
+    for s in shares:  # corrected in place (infectious semantics)
+        assert np.array_equal(s.data, allsh[s.number])
+    # the same inputs through the oracle's per-column decode
+    assert np.array_equal(oracle.FEC(k, n).decode(nums, [r.copy() for r in recv]), data)

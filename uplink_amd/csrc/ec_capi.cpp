@@ -858,6 +858,51 @@ int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, con
     return rc;
 }
 
+// expected[r] = the share numbered nums[outs[r]], re-encoded from the k shares at positions
+// basis[0..k) of the device share slots (rows `slot` apart); expected rows `slot` apart
+static int reencode(ec_ctx *c, const uint8_t *d, size_t slot, size_t len, const int *nums, const int *basis,
+                    const int *outs, int nout, uint8_t *expected, hipStream_t st) {
+    const int k = c->k;
+    std::vector<uint8_t> m((size_t)k * k);
+    for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[basis[i]] * k], k);
+    if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
+    const int ld = round16(nout);
+    std::vector<uint8_t> coef((size_t)k * ld + kCoefPad, 0);
+    for (int r = 0; r < nout; r++)
+        for (int col = 0; col < k; col++) {
+            uint8_t acc = 0;
+            for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[outs[r]] * k + t], m[(size_t)t * k + col]);
+            coef[(size_t)col * ld + r] = acc;
+        }
+    uint8_t *d_coef = nullptr;
+    if (hipMallocAsync(&d_coef, coef.size(), st) != hipSuccess) return EC_ERR_DEVICE;
+    int rc = EC_OK;
+    if (hipMemcpyAsync(d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice, st) != hipSuccess) rc = EC_ERR_DEVICE;
+    if (rc == EC_OK) {
+        RsArgs a{};
+        a.in_base = d;
+        a.out_base = expected;
+        a.coef = d_coef;
+        a.coef_ld = ld;
+        a.in_stripe_stride = (int64_t)len;
+        a.out_stripe_stride = (int64_t)len;
+        a.nin = k;
+        a.nout = nout;
+        for (int j = 0; j < k; j++) {
+            a.in_off[j] = (int64_t)slot * basis[j];
+            a.copy_off[j] = -1;
+        }
+        for (int r = 0; r < nout; r++) a.out_off[r] = (int64_t)slot * r;
+        fill_geometry(a, (int)len, 1, 1);
+        const bool bits = (len % 16) == 0;
+        if (!bits) a.cps = 1;
+        rc = run_matmul(a, 1, bits, st);
+    }
+    // the coefficients must outlive the kernel: the stream-ordered free runs after it
+    (void)hipFreeAsync(d_coef, st);
+    return rc;
+}
+
 int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
@@ -871,87 +916,129 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
     if (k > kMaxOps || nshares - k > kMaxOps) return EC_ERR_UNSUPPORTED;
     const size_t slot = (share_len + 15) & ~(size_t)15;
     const int extra = nshares - k;
+    constexpr int kSample = 64;  // flagged columns decoded first to locate bad shares
     const size_t exp_at = slot * nshares;
     const size_t flags_at = exp_at + slot * (size_t)extra;
     const size_t cols_at = (flags_at + slot + 15) & ~(size_t)15;
     const size_t nums_at = cols_at + share_len * 8;
     const size_t stat_at = nums_at + 4 * 256;
     const size_t out_at = (stat_at + share_len * 4 + 15) & ~(size_t)15;
-    Workspace *w = acquire_ws(c, out_at + share_len * k + 64);
+    const size_t samp_at = (out_at + share_len * k + 15) & ~(size_t)15;  // sample cols, status, changed, row lists
+    const size_t samp_bytes = kSample * (8 + 4 + (size_t)nshares) + 8 * (size_t)nshares + 64;
+    Workspace *w = acquire_ws(c, samp_at + samp_bytes);
     if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
     int rc = EC_OK;
     uint8_t *d = w->d_buf;
+    hipStream_t st = w->stream;
+    auto bw_columns = [&](const std::vector<int64_t> &cl) -> int {  // Berlekamp-Welch on columns, in place
+        if (cl.empty()) return EC_OK;
+        if (hipMemcpyAsync(d + cols_at, cl.data(), cl.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+            launch_berlekamp_welch(d, slot, (const int *)(d + nums_at), k, c->n, nshares,
+                                   (const int64_t *)(d + cols_at), (int)cl.size(), (int *)(d + stat_at), st) !=
+                hipSuccess)
+            return EC_ERR_DEVICE;
+        std::vector<int> status(cl.size());
+        if (hipMemcpyAsync(status.data(), d + stat_at, 4 * cl.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return EC_ERR_DEVICE;
+        for (int s2 : status) {
+            if (s2 == -6) return EC_ERR_NOT_ENOUGH_SHARES;
+            if (s2 == -7) return EC_ERR_TOO_MANY_ERRORS;
+            if (s2 != 0) return EC_ERR_UNSUPPORTED;
+        }
+        return EC_OK;
+    };
     do {
         for (int i = 0; i < nshares; i++)
-            if (hipMemcpyAsync(d + slot * i, shares[i], share_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            if (hipMemcpyAsync(d + slot * i, shares[i], share_len, hipMemcpyHostToDevice, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         if (rc) break;
         if (extra > 0) {
-            // T = G[others] * inverse(G[first k])
-            std::vector<uint8_t> m((size_t)k * k);
-            for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[i] * k], k);
-            if (!gf_invert(m.data(), k)) { rc = EC_ERR_SINGULAR; break; }
-            const int ld = round16(extra);
-            std::vector<uint8_t> coef((size_t)k * ld + kCoefPad, 0);
-            for (int r = 0; r < extra; r++)
-                for (int col = 0; col < k; col++) {
-                    uint8_t acc = 0;
-                    for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[k + r] * k + t], m[(size_t)t * k + col]);
-                    coef[(size_t)col * ld + r] = acc;
-                }
-            uint8_t *d_coef = nullptr;
-            if (hipMalloc(&d_coef, coef.size()) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-            std::unique_ptr<uint8_t, void (*)(uint8_t *)> coef_guard(d_coef, [](uint8_t *p) { (void)hipFree(p); });
-            if (hipMemcpyAsync(d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-            RsArgs a{};
-            a.in_base = d;
-            a.out_base = d + exp_at;
-            a.coef = d_coef;
-            a.coef_ld = ld;
-            a.in_stripe_stride = (int64_t)share_len;
-            a.out_stripe_stride = (int64_t)share_len;
-            a.nin = k;
-            a.nout = extra;
-            for (int j = 0; j < k; j++) { a.in_off[j] = (int64_t)slot * j; a.copy_off[j] = -1; }
-            for (int r = 0; r < extra; r++) a.out_off[r] = (int64_t)slot * r;
-            fill_geometry(a, (int)share_len, 1, 1);
-            const bool bits = (share_len % 16) == 0;
-            if (!bits) a.cps = 1;
-            rc = run_matmul(a, 1, bits, w->stream);
+            // Correct: re-encode the shares beyond the first k from the first k and flag the
+            // columns where any differs
+            std::vector<int> basis(k), rest(extra);
+            for (int i = 0; i < k; i++) basis[i] = i;
+            for (int r = 0; r < extra; r++) rest[r] = k + r;
+            rc = reencode(c, d, slot, share_len, nums, basis.data(), rest.data(), extra, d + exp_at, st);
             if (rc) break;
-            if (launch_flag_columns(d, slot, d + exp_at, slot, k, nshares, share_len, d + flags_at, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            if (launch_flag_columns(d, slot, d + exp_at, slot, k, nshares, share_len, d + flags_at, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
             std::vector<uint8_t> flags(share_len);
-            if (hipMemcpyAsync(flags.data(), d + flags_at, share_len, hipMemcpyDeviceToHost, w->stream) != hipSuccess ||
-                hipStreamSynchronize(w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            if (hipMemcpyAsync(flags.data(), d + flags_at, share_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(d + nums_at, nums, 4 * (size_t)nshares, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
             std::vector<int64_t> cols;
             for (size_t col = 0; col < share_len; col++)
                 if (flags[col]) cols.push_back((int64_t)col);
             if (!cols.empty()) {
-                if (hipMemcpyAsync(d + cols_at, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, w->stream) != hipSuccess ||
-                    hipMemcpyAsync(d + nums_at, nums, 4 * (size_t)nshares, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                if (launch_berlekamp_welch(d, slot, (const int *)(d + nums_at), k, c->n, nshares, (const int64_t *)(d + cols_at),
-                                           (int)cols.size(), (int *)(d + stat_at), w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                std::vector<int> status(cols.size());
-                if (hipMemcpyAsync(status.data(), d + stat_at, 4 * cols.size(), hipMemcpyDeviceToHost, w->stream) != hipSuccess ||
-                    hipStreamSynchronize(w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                for (int st : status) {
-                    if (st == -6) { rc = EC_ERR_NOT_ENOUGH_SHARES; break; }
-                    if (st == -7) { rc = EC_ERR_TOO_MANY_ERRORS; break; }
-                    if (st != 0) { rc = EC_ERR_UNSUPPORTED; break; }
+                // Fast path for errors confined to a few shares (a bad piece): decode a sample of the
+                // flagged columns, take the shares BW rewrote there as the bad set B, and if
+                // |B| <= e check every column on the other shares alone.  Where they agree, the
+                // codeword they define is within e of what was received, so it is the unique BW
+                // answer: B is rewritten from them.  Only columns where they disagree go to BW.
+                bool done = false;
+                const int e = extra / 2;
+                if (e >= 1 && cols.size() > (size_t)4 * kSample) {
+                    std::vector<int64_t> samp(kSample);
+                    for (int i = 0; i < kSample; i++) samp[i] = cols[(size_t)i * cols.size() / kSample];
+                    uint8_t *d_changed = d + samp_at + kSample * 12;
+                    if (hipMemcpyAsync(d + samp_at, samp.data(), kSample * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        launch_berlekamp_welch(d, slot, (const int *)(d + nums_at), k, c->n, nshares,
+                                               (const int64_t *)(d + samp_at), kSample, (int *)(d + samp_at + kSample * 8),
+                                               st, d_changed) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                    std::vector<int> sstat(kSample);
+                    std::vector<uint8_t> changed((size_t)kSample * nshares);
+                    if (hipMemcpyAsync(sstat.data(), d + samp_at + kSample * 8, 4 * kSample, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipMemcpyAsync(changed.data(), d_changed, changed.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                    bool sample_ok = true;
+                    for (int s2 : sstat) sample_ok = sample_ok && s2 == 0;
+                    std::vector<int> bad, good;
+                    for (int i = 0; i < nshares; i++) {
+                        bool b = false;
+                        for (int t = 0; t < kSample && sample_ok; t++) b = b || changed[(size_t)t * nshares + i];
+                        (b ? bad : good).push_back(i);
+                    }
+                    if (sample_ok && !bad.empty() && (int)bad.size() <= e && (int)good.size() >= k) {
+                        // expected rows: the other good shares, then the bad ones, from the first k good
+                        std::vector<int> outs(good.begin() + k, good.end());
+                        const int ncheck = (int)outs.size();
+                        outs.insert(outs.end(), bad.begin(), bad.end());
+                        int *d_rows = (int *)(d_changed + changed.size() + 16 - (changed.size() % 16));
+                        rc = reencode(c, d, slot, share_len, nums, good.data(), outs.data(), (int)outs.size(), d + exp_at, st);
+                        if (rc) break;
+                        if (hipMemcpyAsync(d_rows, outs.data(), 4 * outs.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+                            launch_flag_rows(d, slot, d_rows, ncheck, d + exp_at, slot, share_len, d + flags_at, st) != hipSuccess ||
+                            hipMemcpyAsync(flags.data(), d + flags_at, share_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                            hipStreamSynchronize(st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                        std::vector<int64_t> rest_cols;
+                        for (size_t col = 0; col < share_len; col++)
+                            if (flags[col]) rest_cols.push_back((int64_t)col);
+                        // rewrite the bad shares where the good ones agree, then BW the rest on the
+                        // received data (the sample columns are already decoded: their good
+                        // shares agree now)
+                        if (launch_put_rows(d, slot, d_rows + ncheck, (int)bad.size(), d + exp_at + slot * ncheck, slot,
+                                            share_len, d + flags_at, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                        rc = bw_columns(rest_cols);
+                        if (rc) break;
+                        done = true;
+                    }
                 }
-                if (rc) break;
+                if (!done) {
+                    rc = bw_columns(cols);
+                    if (rc) break;
+                }
                 for (int i = 0; i < nshares; i++)
-                    if (hipMemcpyAsync(shares[i], d + slot * i, share_len, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+                    if (hipMemcpyAsync(shares[i], d + slot * i, share_len, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
                 if (rc) break;
             }
         }
         std::vector<const uint8_t *> dptr(nshares);
         for (int i = 0; i < nshares; i++) dptr[i] = d + slot * i;
-        rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, d + out_at, w->stream);
+        rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, d + out_at, st);
         if (rc) break;
-        if (hipMemcpyAsync(out, d + out_at, share_len * k, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
+        if (hipMemcpyAsync(out, d + out_at, share_len * k, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipStreamSynchronize(st) != hipSuccess) rc = EC_ERR_DEVICE;
     } while (0);
-    if (rc) (void)hipStreamSynchronize(w->stream);
+    if (rc) (void)hipStreamSynchronize(st);
     release_ws(c, w);
     return rc;
 }

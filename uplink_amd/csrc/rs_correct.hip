@@ -10,7 +10,9 @@
 //      e = (r-k)/2 (Gauss-Jordan, free unknowns set to zero), divides Q by E
 //      and rewrites the column with the corrected codeword.  Status per
 //      column: 0, -6 (NotEnoughShares: e <= 0) or -7 (TooManyErrors).
-// Flagged columns are rare (corruption); this path is correctness-first.
+//  rs_flag_rows / rs_put_rows: the fast path of ec_decode when the errors sit
+//      in a few shares (a bad piece): check the other shares against each
+//      other, and rewrite the bad shares from them.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -45,9 +47,31 @@ __global__ void rs_flag_columns(const uint8_t *shares, int64_t stride, const uin
 
 constexpr int kMaxDim = 128;
 
+// rows[0..nrows) of shares against expected rows 0..nrows-1: flag the columns that differ
+__global__ void rs_flag_rows(const uint8_t *shares, int64_t stride, const int *rows, int nrows,
+                             const uint8_t *expected, int64_t estride, int64_t len, uint8_t *flags) {
+    for (int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; col < len;
+         col += (int64_t)gridDim.x * blockDim.x) {
+        uint8_t bad = 0;
+        for (int r = 0; r < nrows; r++)
+            bad |= (uint8_t)(shares[(int64_t)rows[r] * stride + col] != expected[(int64_t)r * estride + col]);
+        flags[col] = bad;
+    }
+}
+
+// shares[rows[r]][col] = expected[r][col] where !skip[col]
+__global__ void rs_put_rows(uint8_t *shares, int64_t stride, const int *rows, int nrows, const uint8_t *expected,
+                            int64_t estride, int64_t len, const uint8_t *skip) {
+    for (int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; col < len;
+         col += (int64_t)gridDim.x * blockDim.x) {
+        if (skip[col]) continue;
+        for (int r = 0; r < nrows; r++) shares[(int64_t)rows[r] * stride + col] = expected[(int64_t)r * estride + col];
+    }
+}
+
 __global__ __launch_bounds__(64) void rs_berlekamp_welch(uint8_t *shares, int64_t stride, const int *nums, int k,
                                                          int n, int ns, const int64_t *cols, int ncols,
-                                                         int *status) {
+                                                         int *status, uint8_t *changed) {
     __shared__ uint8_t A[kMaxDim][kMaxDim + 1];
     __shared__ uint8_t f[kMaxDim];
     __shared__ uint8_t u[kMaxDim];
@@ -143,6 +167,7 @@ __global__ __launch_bounds__(64) void rs_berlekamp_welch(uint8_t *shares, int64_
                     const uint8_t x = dpoint(nums[i]);
                     uint8_t acc = 0;
                     for (int d = k - 1; d >= 0; d--) acc = dmul(acc, x) ^ P[d];
+                    if (changed) changed[(int64_t)ci * ns + i] = shares[(int64_t)i * stride + col] != acc;
                     shares[(int64_t)i * stride + col] = acc;
                 }
             }
@@ -166,11 +191,30 @@ hipError_t launch_flag_columns(const uint8_t *shares, int64_t stride, const uint
 }
 
 hipError_t launch_berlekamp_welch(uint8_t *shares, int64_t stride, const int *nums, int k, int n, int ns,
-                                  const int64_t *cols, int ncols, int *status, hipStream_t s) {
+                                  const int64_t *cols, int ncols, int *status, hipStream_t s, uint8_t *changed) {
     int blocks = ncols < 2048 ? ncols : 2048;
     if (blocks < 1) return hipSuccess;
     hipLaunchKernelGGL(rs_berlekamp_welch, dim3(blocks), dim3(64), 0, s, shares, stride, nums, k, n, ns, cols, ncols,
-                       status);
+                       status, changed);
+    return hipGetLastError();
+}
+
+static int64_t col_blocks(int64_t len) {
+    int64_t b = (len + 255) / 256;
+    return b > 4096 ? 4096 : (b < 1 ? 1 : b);
+}
+
+hipError_t launch_flag_rows(const uint8_t *shares, int64_t stride, const int *rows, int nrows, const uint8_t *expected,
+                            int64_t estride, int64_t len, uint8_t *flags, hipStream_t s) {
+    hipLaunchKernelGGL(rs_flag_rows, dim3((unsigned)col_blocks(len)), dim3(256), 0, s, shares, stride, rows, nrows,
+                       expected, estride, len, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_put_rows(uint8_t *shares, int64_t stride, const int *rows, int nrows, const uint8_t *expected,
+                           int64_t estride, int64_t len, const uint8_t *skip, hipStream_t s) {
+    hipLaunchKernelGGL(rs_put_rows, dim3((unsigned)col_blocks(len)), dim3(256), 0, s, shares, stride, rows, nrows,
+                       expected, estride, len, skip);
     return hipGetLastError();
 }
 
