@@ -221,14 +221,16 @@ class RSScheme:
         ln, datas, nums, ptrs = self._share_arrays(shares)
         k = self.fc.k
         need = k * ln
-        dst = out if (out is not None and out.size >= need) else np.zeros(max(need, 1), dtype=np.uint8)
+        dst = out if (out is not None and out.size >= need) else np.empty(max(need, 1), dtype=np.uint8)
         dst = dst[:need] if need else dst[:0]
-        tmp = np.zeros(max(need, 1), dtype=np.uint8)
-        rc = self._lib.ec_decode(self._ctx, len(shares), nums, ptrs, ln, _ptr(tmp))
+        # written only once the decode has succeeded (the C side copies out last)
+        target = dst if dst.flags["C_CONTIGUOUS"] else np.empty(max(need, 1), dtype=np.uint8)
+        rc = self._lib.ec_decode(self._ctx, len(shares), nums, ptrs, ln, _ptr(target))
         if len(shares) >= k:
             self._resort(shares, nums, ptrs, datas)
         _raise(self._ctx, rc)
-        dst[:] = tmp[:need]
+        if target is not dst:
+            dst[:] = target[:need]
         return dst
 
 
