@@ -31,9 +31,11 @@ struct DecodePlan {
     std::vector<int> missing;  // positions i (== data number) rebuilt
     uint8_t *d_coef = nullptr; // [c][r] = Dinv[missing[r]][c], ld = coef_ld
     int coef_ld = 0;
+    uint64_t *d_tgt = nullptr; // jump-table leaf addresses of d_coef (launch_jt_targets)
     ~DecodePlan() {
         // hipFree synchronises with outstanding device work before releasing
         if (d_coef) (void)hipFree(d_coef);
+        if (d_tgt) (void)hipFree(d_tgt);
     }
 };
 using PlanPtr = std::shared_ptr<DecodePlan>;
@@ -133,6 +135,7 @@ int run_matmul(RsArgs a, int64_t nseg, bool bitsliced, hipStream_t s) {
     int64_t out_off_all[256];
     for (int r = 0; r < total_rows; r++) out_off_all[r] = a.out_off[r];
     const uint8_t *coef0 = a.coef;
+    if (total_rows > kMaxOps) a.jt_tgt = nullptr;  // a prepared table covers one launch of all rows
     int done = 0;
     bool first = true;
     do {
@@ -208,6 +211,16 @@ int get_plan(ec_ctx *c, const std::vector<int> &ids, PlanPtr *out) {
         for (int col = 0; col < k; col++) coef[(size_t)col * p->coef_ld + r] = m[(size_t)p->missing[r] * k + col];
     HIP_TRY(hipMalloc(&p->d_coef, coef.size()));
     HIP_TRY(hipMemcpy(p->d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice));
+    if (R > 0 && R <= kMaxOps) {  // the generic kernel's leaf addresses, made once per plan
+        RsArgs t{};
+        t.coef = p->d_coef;
+        t.coef_ld = p->coef_ld;
+        t.nin = k;
+        t.nout = R;
+        HIP_TRY(hipMalloc(&p->d_tgt, jt_targets_bytes(t)));
+        HIP_TRY(launch_jt_targets(t, p->d_tgt, nullptr));
+        HIP_TRY(hipStreamSynchronize(nullptr));
+    }
     {
         std::lock_guard<std::mutex> g(c->mu);
         c->plans.push_front(p);
@@ -236,6 +249,7 @@ int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const
     a.out_base = out;
     a.coef = plan->d_coef;
     a.coef_ld = plan->coef_ld;
+    a.jt_tgt = plan->d_tgt;
     a.in_stripe_stride = ess;
     a.out_stripe_stride = (int64_t)k * ess;
     a.in_seg_stride = piece_seg_stride;

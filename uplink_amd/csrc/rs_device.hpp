@@ -217,18 +217,19 @@ typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
 // acc[O] ^= D[row O][j] * x_j for the wave's 8 - skip accumulator rows.
 // xa = LDS byte address of plane 0 of x_j for this lane (plane p at +256 p);
-// ca = LDS address of the 8 16-bit leaf offsets (coefficient * RS_JT_SLOT)
-// of the wave's rows for j, right-aligned (slot skip + i holds row i).
-// The planes land directly in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8];
-// 22 XORs fill the other combinations; the 8 leaf addresses are formed up
-// front (s[52:67]); then, with VGPR index mode on for the accumulator operand
-// (SRC0 and DST, M0 = 8 * row, stepped by each leaf), a jump enters the
-// sequence of eight s_swappc_b64 (4 bytes each) at call site `skip`, so only
-// the wave's rows are visited; the leaves return with s_setpc_b64.
+// tp = the 8 absolute leaf addresses of the wave's rows for j, right-aligned
+// (entry skip + i holds row i), in global memory (rs_jt_targets).  One scalar
+// load brings them straight into the call registers s[52:67] while the planes
+// land in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8]; 22 XORs fill the
+// other combinations; then, with VGPR index mode on for the accumulator
+// operand (SRC0 and DST, M0 = 8 * row, stepped by each leaf), a jump enters
+// the sequence of eight s_swappc_b64 (4 bytes each) at call site `skip`, so
+// only the wave's rows are visited; the leaves return with s_setpc_b64.
 // Registers are fixed by the register contract of rs_jump_table.inc: acc in
-// v[32:95] (pinned operands), combinations v[96:125], s[40:67] scratch.
-__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t ca, uint32_t skip) {
+// v[32:95] (pinned operands), combinations v[96:125], s[42:67] scratch.
+__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, const uint64_t *tp, uint32_t skip) {
     asm volatile(
+        "s_load_dwordx16 s[52:67], %[tp], 0x0\n"
         "s_mov_b32 s51, m0\n"
         "ds_read_b32 v96, %[xa]\n"
         "ds_read_b32 v97, %[xa] offset:256\n"
@@ -238,16 +239,14 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         "ds_read_b32 v112, %[xa] offset:1280\n"
         "ds_read_b32 v114, %[xa] offset:1536\n"
         "ds_read_b32 v118, %[xa] offset:1792\n"
-        "ds_read_b128 v[104:107], %[ca]\n"
-        "s_getpc_b64 s[40:41]\n"
+        "s_getpc_b64 s[42:43]\n"
         ".Ljt_pc%=:\n"
-        "s_add_u32 s40, s40, .Ljt_tab%=-.Ljt_pc%=\n"
-        "s_addc_u32 s41, s41, 0\n"
+        "s_lshl_b32 s50, %[skip], 2\n"
+        "s_add_u32 s42, s42, s50\n"
+        "s_addc_u32 s43, s43, 0\n"
+        "s_add_u32 s42, s42, .Ljt_sites%=-.Ljt_pc%=\n"
+        "s_addc_u32 s43, s43, 0\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_readfirstlane_b32 s44, v104\n"
-        "v_readfirstlane_b32 s45, v105\n"
-        "v_readfirstlane_b32 s46, v106\n"
-        "v_readfirstlane_b32 s47, v107\n"
         "v_xor_b32 v98, v96, v97\n"
         "v_xor_b32 v100, v96, v99\n"
         "v_xor_b32 v101, v97, v99\n"
@@ -270,37 +269,6 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         "v_xor_b32 v123, v115, v118\n"
         "v_xor_b32 v124, v116, v118\n"
         "v_xor_b32 v125, v117, v118\n"
-        "s_and_b32 s50, s44, 0xffff\n"
-        "s_add_u32 s52, s40, s50\n"
-        "s_addc_u32 s53, s41, 0\n"
-        "s_lshr_b32 s50, s44, 16\n"
-        "s_add_u32 s54, s40, s50\n"
-        "s_addc_u32 s55, s41, 0\n"
-        "s_and_b32 s50, s45, 0xffff\n"
-        "s_add_u32 s56, s40, s50\n"
-        "s_addc_u32 s57, s41, 0\n"
-        "s_lshr_b32 s50, s45, 16\n"
-        "s_add_u32 s58, s40, s50\n"
-        "s_addc_u32 s59, s41, 0\n"
-        "s_and_b32 s50, s46, 0xffff\n"
-        "s_add_u32 s60, s40, s50\n"
-        "s_addc_u32 s61, s41, 0\n"
-        "s_lshr_b32 s50, s46, 16\n"
-        "s_add_u32 s62, s40, s50\n"
-        "s_addc_u32 s63, s41, 0\n"
-        "s_and_b32 s50, s47, 0xffff\n"
-        "s_add_u32 s64, s40, s50\n"
-        "s_addc_u32 s65, s41, 0\n"
-        "s_lshr_b32 s50, s47, 16\n"
-        "s_add_u32 s66, s40, s50\n"
-        "s_addc_u32 s67, s41, 0\n"
-        "s_getpc_b64 s[42:43]\n"
-        ".Ljt_pc2%=:\n"
-        "s_lshl_b32 s50, %[skip], 2\n"
-        "s_add_u32 s42, s42, s50\n"
-        "s_addc_u32 s43, s43, 0\n"
-        "s_add_u32 s42, s42, .Ljt_sites%=-.Ljt_pc2%=\n"
-        "s_addc_u32 s43, s43, 0\n"
         "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
         "s_setpc_b64 s[42:43]\n"
         ".Ljt_sites%=:\n"
@@ -314,18 +282,37 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, uint32_t 
         "s_swappc_b64 s[48:49], s[66:67]\n"
         "s_set_gpr_idx_off\n"
         "s_mov_b32 m0, s51\n"
-        "s_branch .Ljt_end%=\n"
-        ".Ljt_tab%=:\n"
-        RS_JUMP_TABLE_ASM
-        ".Ljt_end%=:\n"
         : "+{v[32:39]}"(acc[0]), "+{v[40:47]}"(acc[1]), "+{v[48:55]}"(acc[2]), "+{v[56:63]}"(acc[3]),
           "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7])
-        : [xa] "v"(xa), [ca] "v"(ca), [skip] "s"(skip)
+        : [xa] "v"(xa), [tp] "s"(tp), [skip] "s"(skip)
         : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
           "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
-          "v122", "v123", "v124", "v125", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51",
+          "v122", "v123", "v124", "v125", "s42", "s43", "s48", "s49", "s50", "s51",
           "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
           "s67", "scc", "memory");
+}
+
+// Absolute address of leaf 0 of the jump table.  The table itself sits here,
+// behind a branch, in the code of the one kernel that calls this
+// (rs_jt_targets); the leaves are position-independent code that any kernel
+// honouring the register contract calls through the addresses it computes.
+__device__ __forceinline__ uint64_t jt_table_base() {
+    uint32_t lo, hi;
+    asm volatile(
+        "s_getpc_b64 s[40:41]\n"
+        ".Ltb_pc%=:\n"
+        "s_add_u32 s40, s40, .Ltb_tab%=-.Ltb_pc%=\n"
+        "s_addc_u32 s41, s41, 0\n"
+        "s_mov_b32 %0, s40\n"
+        "s_mov_b32 %1, s41\n"
+        "s_branch .Ltb_end%=\n"
+        ".Ltb_tab%=:\n"
+        RS_JUMP_TABLE_ASM
+        ".Ltb_end%=:\n"
+        : "=s"(lo), "=s"(hi)
+        :
+        : "s40", "s41", "scc");
+    return ((uint64_t)hi << 32) | lo;
 }
 
 }  // namespace dev

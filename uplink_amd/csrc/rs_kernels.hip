@@ -106,9 +106,10 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
 // and the row group of a wave is rotated by
 // blockIdx so the SIMDs of a CU, which host waves of several workgroups, get
 // equal VALU work.  Each coefficient is multiplied in through the jump table
-// (jt_input): the LDS copy of the matrix holds leaf offsets c * RS_JT_SLOT as
-// [pass][j][group][8] 16-bit words (0 = empty leaf for padded rows), built
-// once per workgroup; jt_lds_bytes() gives the dynamic LDS size.
+// (jt_input), whose 8 leaf addresses per (pass, j, wave row group) come
+// from the table rs_jt_targets made (a.jt_tgt, [pass][j][group][8] 64-bit
+// words; leaf 0 = empty for padded rows); jt_lds_bytes() gives the dynamic
+// LDS size.
 constexpr int kJtRows = 8;  // accumulator rows per wave
 
 template <int NW>
@@ -116,25 +117,11 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *lds = smem;                                  // 2 x [JC][8 planes][64 lanes]
-    uint16_t *lco = (uint16_t *)(smem + 2 * JC * 8 * 64);  // leaf offsets
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
-    {
-        const int per_pass = a.nin * NW * OPW;
-        for (int t = threadIdx.x; t < npass * per_pass; t += NW * 64) {
-            const int pass = t / per_pass, r = t - pass * per_pass;
-            const int j = r / (NW * OPW), g = (r / OPW) % NW, o = r % OPW;
-            const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
-            const int rb = p0 + g * prow / NW, cn = p0 + (g + 1) * prow / NW - rb;
-            const int oo = o - (OPW - cn);  // rows right-aligned: jt_input enters at call site OPW - cnt
-            lco[t] = oo >= 0 ? (uint16_t)(a.coef[(int64_t)j * a.coef_ld + rb + oo] * RS_JT_SLOT) : (uint16_t)0;
-        }
-    }
-    __syncthreads();
     const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 4;
-    const uint32_t lco_addr = (uint32_t)(uintptr_t)lco;
     // Plane chunks alternate between two LDS buffers, so one barrier per chunk
     // suffices: a wave staging chunk c+1 has passed barrier c, which every wave
     // reached only after it finished reading chunk c-1 from that buffer.
@@ -157,7 +144,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 #pragma nounroll
                     for (int jj = 0; jj < jn; jj++)
                         jt_input(acc, lds_addr + (uint32_t)((buf * JC + jj) * 8 * 64 * 4),
-                                 lco_addr + (uint32_t)((((pass * a.nin + j0 + jj) * NW + group) * OPW) * 2),
+                                 a.jt_tgt + ((pass * a.nin + j0 + jj) * NW + group) * OPW,
                                  (uint32_t)(OPW - cnt));
                 }
                 buf ^= 1;
@@ -173,9 +160,29 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 }
 
 template <int NW>
-size_t jt_lds_bytes(const RsArgs &a) {
-    const int npass = a.nout > 0 ? (a.nout + NW * kJtRows - 1) / (NW * kJtRows) : 1;
-    return (size_t)2 * 2 * NW * 8 * 64 * 4 + (size_t)npass * a.nin * NW * kJtRows * 2;
+size_t jt_lds_bytes(const RsArgs &) {
+    return (size_t)2 * 2 * NW * 8 * 64 * 4;
+}
+
+int jt_waves(int nout) { return nout <= 2 * kJtRows ? 2 : nout <= 3 * kJtRows ? 3 : 4; }
+
+// Leaf addresses of the matrix for rs_matmul_jt<nw>: the rows of each pass
+// split over the nw row groups exactly as that kernel splits them, right-
+// aligned in 8 slots (jt_input enters at call site 8 - count).
+__global__ __launch_bounds__(256) void rs_jt_targets(const RsArgs a, int nw, uint64_t *tgt) {
+    const uint64_t base = jt_table_base();
+    constexpr int OPW = kJtRows;
+    const int npass = a.nout > 0 ? (a.nout + nw * OPW - 1) / (nw * OPW) : 1;
+    const int per_pass = a.nin * nw * OPW;
+    for (int t = threadIdx.x; t < npass * per_pass; t += blockDim.x) {
+        const int pass = t / per_pass, r = t - pass * per_pass;
+        const int j = r / (nw * OPW), g = (r / OPW) % nw, o = r % OPW;
+        const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
+        const int rb = p0 + g * prow / nw, cn = p0 + (g + 1) * prow / nw - rb;
+        const int oo = o - (OPW - cn);
+        const uint32_t c = oo >= 0 ? a.coef[(int64_t)j * a.coef_ld + rb + oo] : 0u;
+        tgt[t] = base + (uint64_t)c * RS_JT_SLOT;
+    }
 }
 
 // ------------------------------------------------ byte-wise fallback
@@ -267,21 +274,48 @@ hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStr
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
+size_t jt_targets_bytes(const RsArgs &a) {
+    const int nw = jt_waves(a.nout);
+    const int npass = a.nout > 0 ? (a.nout + nw * kJtRows - 1) / (nw * kJtRows) : 1;
+    return (size_t)npass * a.nin * nw * kJtRows * sizeof(uint64_t);
+}
+
+hipError_t launch_jt_targets(const RsArgs &a, uint64_t *targets, hipStream_t s) {
+    hipLaunchKernelGGL(rs_jt_targets, dim3(1), dim3(256), 0, s, a, jt_waves(a.nout), targets);
+    return hipGetLastError();
+}
+
+hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t s) {
+    RsArgs a = args;
+    uint64_t *own = nullptr;
+    if (!a.jt_tgt) {  // no prepared table: make one for this launch (stream-ordered)
+        hipError_t e = hipMallocAsync((void **)&own, jt_targets_bytes(a), s);
+        if (e != hipSuccess) return e;
+        if ((e = launch_jt_targets(a, own, s)) != hipSuccess) {
+            (void)hipFreeAsync(own, s);
+            return e;
+        }
+        a.jt_tgt = own;
+    }
     // up to 16 waves per CU (4 per SIMD: the jump-table body holds ~126
     // VGPRs); as few waves per workgroup as the rows need, since every wave
     // rebuilds the 4-plane combinations of each input for its own rows
-    if (a.nout <= 2 * kJtRows) {
+    switch (jt_waves(a.nout)) {
+    case 2:
         if (grid <= 0) grid = default_grid(a.total_tiles, 8);
         hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);
-    } else if (a.nout <= 3 * kJtRows) {
+        break;
+    case 3:
         if (grid <= 0) grid = default_grid(a.total_tiles, 5);
         hipLaunchKernelGGL((rs_matmul_jt<3>), dim3(grid), dim3(3 * 64), jt_lds_bytes<3>(a), s, a);
-    } else {
+        break;
+    default:
         if (grid <= 0) grid = default_grid(a.total_tiles, 4);
         hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
     }
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (own) (void)hipFreeAsync(own, s);  // runs after the kernel on s
+    return e;
 }
 
 hipError_t launch_matmul_bytes(const RsArgs &a, hipStream_t s) {

@@ -33,6 +33,7 @@ struct RsArgs {
     const uint8_t *in_base;
     uint8_t *out_base;
     const uint8_t *coef;      // runtime matrix, coef[j*coef_ld + r] (generic kernel)
+    const uint64_t *jt_tgt;   // leaf addresses of coef (jt_targets_bytes; null: made per launch)
     int64_t in_stripe_stride;
     int64_t out_stripe_stride;
     int64_t in_seg_stride;
@@ -59,6 +60,13 @@ bool have_special_encoder(int k, int n);
 // any matrix for the generic kernel.  Return hipError_t.
 hipError_t launch_encode_special(int k, int n, const RsArgs &args, int grid, hipStream_t stream);
 hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t stream);
+// The generic kernel multiplies through a jump table whose leaf addresses
+// depend on the matrix: launch_jt_targets writes them for args.coef / nin /
+// nout into `targets` (jt_targets_bytes(args) bytes of device memory), after
+// which args.jt_tgt = targets lets any number of launches of that matrix skip
+// the per-launch preparation.
+size_t jt_targets_bytes(const RsArgs &args);
+hipError_t launch_jt_targets(const RsArgs &args, uint64_t *targets, hipStream_t stream);
 // Byte-wise fallback (any ess, any alignment); coef as above.
 hipError_t launch_matmul_bytes(const RsArgs &args, hipStream_t stream);
 
