@@ -215,22 +215,37 @@ __device__ __forceinline__ void compute_special(const uint32_t *lds, int lane, u
 
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
-// acc[O] ^= D[row O][j] * x_j for the wave's 8 - skip accumulator rows.
-// xa = LDS byte address of plane 0 of x_j for this lane (plane p at +256 p);
-// tp = the 8 absolute leaf addresses of the wave's rows for j, right-aligned
-// (entry skip + i holds row i), in global memory (rs_jt_targets).  One scalar
-// load brings them straight into the call registers s[52:67] while the planes
-// land in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8]; 22 XORs fill the
-// other combinations; then, with VGPR index mode on for the accumulator
-// operand (SRC0 and DST, M0 = 8 * row, stepped by each leaf), a jump enters
-// the sequence of eight s_swappc_b64 (4 bytes each) at call site `skip`, so
-// only the wave's rows are visited; the leaves return with s_setpc_b64.
-// Registers are fixed by the register contract of rs_jump_table.inc: acc in
-// v[32:95] (pinned operands), combinations v[96:125], s[42:67] scratch.
-__device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, const uint64_t *tp, uint32_t skip) {
+// acc[O] ^= sum over the n inputs j of D[row O][j] * x_j, for the wave's
+// 8 - skip accumulator rows.  xa = LDS byte address of plane 0 of the first
+// input for this lane (plane p at +256 p, the next input 2 KiB on); tp = the
+// first input's 8 absolute leaf addresses of the wave's rows, right-aligned
+// (entry skip + i holds row i), in global memory (rs_jt_targets), the next
+// input's `tstride` bytes on.  Per input, one scalar load brings the leaf
+// addresses straight into the call registers s[52:67] while the planes land
+// in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8]; 22 XORs fill the other
+// combinations; then, with VGPR index mode on for the accumulator operand
+// (SRC0 and DST, M0 = 8 * row, stepped by each leaf), a jump enters the
+// sequence of eight s_swappc_b64 (4 bytes each) at call site `skip`, so only
+// the wave's rows are visited; the leaves return with s_setpc_b64.  The loop
+// over the inputs is part of the asm, so the call-site entry and M0 are set
+// up once per chunk.  Registers are fixed by the register contract of
+// rs_jump_table.inc: acc in v[32:95] (pinned operands), combinations
+// v[96:125], s[42:67] scratch.  n >= 1.
+__device__ __forceinline__ void jt_inputs(u32x8 (&acc)[8], uint32_t xa, const uint64_t *tp, uint32_t tstride,
+                                          uint32_t skip, uint32_t n) {
     asm volatile(
         "s_load_dwordx16 s[52:67], %[tp], 0x0\n"
+        "s_mov_b64 s[44:45], %[tp]\n"
+        "s_mov_b32 s46, %[n]\n"
         "s_mov_b32 s51, m0\n"
+        "s_getpc_b64 s[42:43]\n"
+        ".Ljt_pc%=:\n"
+        "s_lshl_b32 s50, %[skip], 2\n"
+        "s_add_u32 s42, s42, s50\n"
+        "s_addc_u32 s43, s43, 0\n"
+        "s_add_u32 s42, s42, .Ljt_sites%=-.Ljt_pc%=\n"
+        "s_addc_u32 s43, s43, 0\n"
+        ".Ljt_loop%=:\n"
         "ds_read_b32 v96, %[xa]\n"
         "ds_read_b32 v97, %[xa] offset:256\n"
         "ds_read_b32 v99, %[xa] offset:512\n"
@@ -239,13 +254,10 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, const uin
         "ds_read_b32 v112, %[xa] offset:1280\n"
         "ds_read_b32 v114, %[xa] offset:1536\n"
         "ds_read_b32 v118, %[xa] offset:1792\n"
-        "s_getpc_b64 s[42:43]\n"
-        ".Ljt_pc%=:\n"
-        "s_lshl_b32 s50, %[skip], 2\n"
-        "s_add_u32 s42, s42, s50\n"
-        "s_addc_u32 s43, s43, 0\n"
-        "s_add_u32 s42, s42, .Ljt_sites%=-.Ljt_pc%=\n"
-        "s_addc_u32 s43, s43, 0\n"
+        "v_add_u32 %[xa], 0x800, %[xa]\n"
+        "s_add_u32 s44, s44, %[ts]\n"
+        "s_addc_u32 s45, s45, 0\n"
+        "s_sub_u32 s46, s46, 1\n"
         "s_waitcnt lgkmcnt(0)\n"
         "v_xor_b32 v98, v96, v97\n"
         "v_xor_b32 v100, v96, v99\n"
@@ -281,13 +293,18 @@ __device__ __forceinline__ void jt_input(u32x8 (&acc)[8], uint32_t xa, const uin
         "s_swappc_b64 s[48:49], s[64:65]\n"
         "s_swappc_b64 s[48:49], s[66:67]\n"
         "s_set_gpr_idx_off\n"
+        "s_cmp_eq_u32 s46, 0\n"
+        "s_cbranch_scc1 .Ljt_done%=\n"
+        "s_load_dwordx16 s[52:67], s[44:45], 0x0\n"
+        "s_branch .Ljt_loop%=\n"
+        ".Ljt_done%=:\n"
         "s_mov_b32 m0, s51\n"
         : "+{v[32:39]}"(acc[0]), "+{v[40:47]}"(acc[1]), "+{v[48:55]}"(acc[2]), "+{v[56:63]}"(acc[3]),
-          "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7])
-        : [xa] "v"(xa), [tp] "s"(tp), [skip] "s"(skip)
+          "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7]), [xa] "+v"(xa)
+        : [tp] "s"(tp), [ts] "s"(tstride), [skip] "s"(skip), [n] "s"(n)
         : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108",
           "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121",
-          "v122", "v123", "v124", "v125", "s42", "s43", "s48", "s49", "s50", "s51",
+          "v122", "v123", "v124", "v125", "s42", "s43", "s44", "s45", "s46", "s48", "s49", "s50", "s51",
           "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
           "s67", "scc", "memory");
 }

@@ -102,11 +102,11 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
 // specialised kernel).  Every wave computes (no loader waves) and several
 // workgroups share a CU; inputs are staged in LDS chunks of 2*NW shares.
 // The rows of a pass are spread evenly over the NW waves (<= 8 each, the
-// accumulators of jt_input), each wave stages two inputs of a chunk of 2*NW,
+// accumulators of jt_inputs), each wave stages two inputs of a chunk of 2*NW,
 // and the row group of a wave is rotated by
 // blockIdx so the SIMDs of a CU, which host waves of several workgroups, get
 // equal VALU work.  Each coefficient is multiplied in through the jump table
-// (jt_input), whose 8 leaf addresses per (pass, j, wave row group) come
+// (jt_inputs), whose 8 leaf addresses per (pass, j, wave row group) come
 // from the table rs_jt_targets made (a.jt_tgt, [pass][j][group][8] 64-bit
 // words; leaf 0 = empty for padded rows); jt_lds_bytes() gives the dynamic
 // LDS size.
@@ -140,13 +140,10 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
                 stage_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0);
                 lds_barrier();
-                if (cnt > 0) {
-#pragma nounroll
-                    for (int jj = 0; jj < jn; jj++)
-                        jt_input(acc, lds_addr + (uint32_t)((buf * JC + jj) * 8 * 64 * 4),
-                                 a.jt_tgt + ((pass * a.nin + j0 + jj) * NW + group) * OPW,
-                                 (uint32_t)(OPW - cnt));
-                }
+                if (cnt > 0)
+                    jt_inputs(acc, lds_addr + (uint32_t)(buf * JC * 8 * 64 * 4),
+                              a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
+                              (uint32_t)(OPW - cnt), (uint32_t)jn);
                 buf ^= 1;
             }
             uint32_t rows[OPW][8];
@@ -168,7 +165,7 @@ int jt_waves(int nout) { return nout <= 2 * kJtRows ? 2 : nout <= 3 * kJtRows ? 
 
 // Leaf addresses of the matrix for rs_matmul_jt<nw>: the rows of each pass
 // split over the nw row groups exactly as that kernel splits them, right-
-// aligned in 8 slots (jt_input enters at call site 8 - count).
+// aligned in 8 slots (jt_inputs enters at call site 8 - count).
 __global__ __launch_bounds__(256) void rs_jt_targets(const RsArgs a, int nw, uint64_t *tgt) {
     const uint64_t base = jt_table_base();
     constexpr int OPW = kJtRows;
