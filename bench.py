@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--settle-s", type=float, default=0.3,
                     help="untimed steps run for at least this long before the W warm-up steps: the chip's clocks "
                          "ramp for tens of ms under sustained load (DESIGN.md §5)")
-    ap.add_argument("--batch", type=int, default=8, help="segments per step per GPU")
+    ap.add_argument("--batch", type=int, default=16,
+                    help="segments per step per GPU (12-16 measured best on MI355X, DESIGN.md §5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-segments", type=int, default=4)
     ap.add_argument("--cpu-sample-s", type=float, default=10.0,
@@ -275,7 +276,8 @@ def main():
     try:
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        traffic = tj.get(dominant, {}).get("hbm_bytes_per_launch")
+        if tj.get("segments_per_launch", 8) == B:  # PMC bytes are per launch of this batch size
+            traffic = tj.get(dominant, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     line = {

@@ -10,7 +10,8 @@ import sys
 from collections import defaultdict
 
 fetch_dir, write_dir, out = sys.argv[1:4]
-K, N, S_PAD, B = 29, 80, 9040 * 29 * 256, 8
+B = int(sys.argv[4]) if len(sys.argv) > 4 else 16  # segments per launch (bench.py --batch)
+K, N, S_PAD = 29, 80, 9040 * 29 * 256
 
 
 def per_kernel(d, counter):
@@ -43,10 +44,11 @@ def family(match):
 
 
 res = {
-    "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of `python3 bench.py "
-              "--steps 3 --warmup 1 --settle-s 0 --no-cpu-baseline` (8 RS(29,80) 64 MiB segments per launch); mean "
+    "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of `python3 bench.py "
+              f"--steps 3 --warmup 1 --settle-s 0 --no-cpu-baseline` ({B} RS(29,80) 64 MiB segments per launch); mean "
               "over dispatches; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py",
-    "encode": family("rs_encode_special"),
+    "segments_per_launch": B,
+    "encode": family("rs_encode_special<29, 80, 4, 4>"),
     "decode": family("rs_matmul_jt"),
     "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD},
 }
