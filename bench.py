@@ -5,7 +5,7 @@ BASELINE.json metric on configs[1]+configs[2], batched as
 C4 (independent segments, sharded across ranks with no collective on the data
 path: weak scaling).
 
-One step on each rank = one batch of `--batch` (default 8) distinct synthetic
+One step on each rank = one batch of `--batch` (default 16) distinct synthetic
 64 MiB segments (PadReader-padded to 9040 stripes x 29 x 256 B, stripe-major,
 resident in HBM):
   1. ec_encode_segments: every segment -> 80 pieces of 2,314,240 B
