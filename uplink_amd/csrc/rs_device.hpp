@@ -149,55 +149,6 @@ __device__ __forceinline__ void stage_inputs(const RsArgs &a, int64_t seg, const
     }
 }
 
-// stage_inputs split in two, so a kernel can issue the global loads of its
-// next chunk before it computes on the current one: load_inputs fills the
-// registers, slice_inputs copies through / bit-slices / writes LDS.
-template <int PER>
-struct StageRegs {
-    uint4 A[PER], B[PER];
-};
-
-template <int NW, int PER, bool NT = false>
-__device__ __forceinline__ void load_inputs(const RsArgs &a, int64_t seg, const TileCols &c, int wave, int j0, int jn,
-                                            StageRegs<PER> &r) {
-    // Columns past the end of the segment load column 0 instead of branching:
-    // their planes are never stored (slice_inputs and store_rows test vA/vB).
-    const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
-    const int64_t oA = c.vA ? c.inA : 0, oB = c.vB ? c.inB : 0;
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const int j = wave + NW * i;
-        if (j < jn) {
-            const uint8_t *p = in_seg + a.in_off[j0 + j];
-            r.A[i] = ld16<NT>(p + oA);
-            r.B[i] = ld16<NT>(p + oB);
-        }
-    }
-}
-
-template <int NW, int PER, bool NT = false>
-__device__ __forceinline__ void slice_inputs(const RsArgs &a, int64_t seg, const TileCols &c, uint32_t *lds, int lane,
-                                             int wave, int j0, int jn, bool do_copy, const StageRegs<PER> &r) {
-    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
-#pragma unroll
-    for (int i = 0; i < PER; i++) {
-        const int j = wave + NW * i;
-        if (j < jn) {
-            const int64_t co = a.copy_off[j0 + j];
-            if (do_copy && co >= 0) {
-                uint8_t *p = out_seg + co;
-                if (c.vA) st16<NT>(p + c.outA, r.A[i].x, r.A[i].y, r.A[i].z, r.A[i].w);
-                if (c.vB) st16<NT>(p + c.outB, r.B[i].x, r.B[i].y, r.B[i].z, r.B[i].w);
-            }
-            uint32_t w[8] = {r.A[i].x, r.A[i].y, r.A[i].z, r.A[i].w, r.B[i].x, r.B[i].y, r.B[i].z, r.B[i].w};
-            bitslice8(w);
-            uint32_t *dst = lds + j * 8 * 64 + lane;
-#pragma unroll
-            for (int p = 0; p < 8; p++) dst[p * 64] = w[p];
-        }
-    }
-}
-
 // Output: un-bit-slice each accumulated row and store its two chunks.
 template <int OPW, bool NT = false>
 __device__ __forceinline__ void store_rows(const RsArgs &a, int64_t seg, const TileCols &c, int rbase, int cnt,

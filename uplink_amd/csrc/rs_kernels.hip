@@ -136,17 +136,10 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             u32x8 acc[OPW];
 #pragma unroll
             for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
-            StageRegs<PER> r;
-            load_inputs<NW, PER, true>(a, seg, c, wave, 0, a.nin < JC ? a.nin : JC, r);
             for (int j0 = 0; j0 < a.nin; j0 += JC) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
-                slice_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
+                stage_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0);
                 lds_barrier();
-                // The next chunk's loads are in flight while this chunk is multiplied in.
-                if (j0 + JC < a.nin) {
-                    const int j1 = j0 + JC;
-                    load_inputs<NW, PER, true>(a, seg, c, wave, j1, a.nin - j1 < JC ? a.nin - j1 : JC, r);
-                }
                 if (cnt > 0)
                     jt_inputs(acc, lds_addr + (uint32_t)(buf * JC * 8 * 64 * 4),
                               a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
