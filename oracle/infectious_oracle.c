@@ -550,6 +550,99 @@ int or_baseline_rebuild_segment(int k, int n, int ess, const uint8_t *enc, int n
     return rc;
 }
 
+/* The optimised CPU variant of the same two loops (SURVEY §8d "all rows per
+ * stripe"), reported next to the reference-shaped baseline: threads split the
+ * stripes; each thread walks blocks of 32 stripes (~230 KB of input, L2-resident)
+ * and produces every piece's share of them, so each input byte is read from
+ * memory once instead of once per piece; the rebuild inverts once per share
+ * set instead of once per stripe.  Same results as the reference-shaped
+ * loops (tests/test_oracle.py). */
+typedef struct {
+    int k, n, ess; const uint8_t *enc; const uint8_t *seg; size_t nstripes; uint8_t *pieces;
+    size_t s0, s1;
+    const uint8_t *dmat; const int *ids; const uint8_t *const *src; uint8_t *out;  /* rebuild */
+} fast_job;
+
+static void *fast_enc_worker(void *arg) {
+    fast_job *j = (fast_job *)arg;
+    const size_t stripe = (size_t)j->k * j->ess, plen = j->nstripes * j->ess, blk = 32;
+    for (size_t b0 = j->s0; b0 < j->s1; b0 += blk) {
+        const size_t b1 = b0 + blk < j->s1 ? b0 + blk : j->s1;
+        for (int num = 0; num < j->n; num++) {
+            for (size_t s = b0; s < b1; s++) {
+                const uint8_t *in = j->seg + s * stripe;
+                uint8_t *o = j->pieces + (size_t)num * plen + s * j->ess;
+                if (num < j->k) { memcpy(o, in + (size_t)num * j->ess, j->ess); continue; }
+                memset(o, 0, j->ess);
+                for (int i = 0; i < j->k; i++) addmul(o, in + (size_t)i * j->ess, j->enc[(size_t)num * j->k + i], j->ess);
+            }
+        }
+    }
+    return NULL;
+}
+
+int or_fast_encode_segment(int k, int n, int ess, const uint8_t *enc, const uint8_t *seg, size_t nstripes,
+                           uint8_t *pieces, int threads) {
+    or_init();
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    fast_job *jobs = (fast_job *)calloc(threads, sizeof(fast_job));
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (fast_job){k, n, ess, enc, seg, nstripes, pieces, nstripes * t / threads, nstripes * (t + 1) / threads,
+                             NULL, NULL, NULL, NULL};
+        pthread_create(&th[t], NULL, fast_enc_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs);
+    return 0;
+}
+
+static void *fast_dec_worker(void *arg) {
+    fast_job *j = (fast_job *)arg;
+    const size_t stripe = (size_t)j->k * j->ess;
+    for (size_t s = j->s0; s < j->s1; s++) {
+        uint8_t *o = j->out + s * stripe;
+        for (int i = 0; i < j->k; i++) {
+            uint8_t *dst = o + (size_t)i * j->ess;
+            if (j->ids[i] < j->k) { memcpy(o + (size_t)j->ids[i] * j->ess, j->src[i] + s * j->ess, j->ess); continue; }
+            memset(dst, 0, j->ess);
+            for (int c = 0; c < j->k; c++) addmul(dst, j->src[c] + s * j->ess, j->dmat[(size_t)i * j->k + c], j->ess);
+        }
+    }
+    return NULL;
+}
+
+/* Rebuild from exactly k pieces (numbers `nums`, any order): one share choice
+ * and one inversion, then every stripe. */
+int or_fast_rebuild_segment(int k, int n, int ess, const uint8_t *enc, const int *nums, const uint8_t *const *pieces,
+                            size_t nstripes, uint8_t *out, int threads) {
+    or_init();
+    int numbers[256]; const uint8_t *data[256]; int ids[256]; const uint8_t *src[256];
+    for (int i = 0; i < k; i++) { numbers[i] = nums[i]; data[i] = pieces[i]; }
+    sort_shares(k, numbers, data);
+    uint8_t *m = (uint8_t *)calloc((size_t)k * k, 1);
+    int b = 0, e = k - 1;
+    for (int i = 0; i < k; i++) {
+        if (numbers[b] == i) { ids[i] = numbers[b]; src[i] = data[b]; b++; }
+        else { ids[i] = numbers[e]; src[i] = data[e]; e--; }
+        if (ids[i] >= n || ids[i] < 0) { free(m); return -11; }
+        if (ids[i] < k) m[(size_t)i * (k + 1)] = 1;
+        else memcpy(m + (size_t)i * k, enc + (size_t)ids[i] * k, k);
+    }
+    if (or_invert_matrix(m, k) != 0) { free(m); return -12; }
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    fast_job *jobs = (fast_job *)calloc(threads, sizeof(fast_job));
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (fast_job){k, n, ess, enc, NULL, nstripes, NULL, nstripes * t / threads, nstripes * (t + 1) / threads,
+                             m, ids, src, out};
+        pthread_create(&th[t], NULL, fast_dec_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs); free(m);
+    return 0;
+}
+
 /* ------------------------------------------------------------- padding */
 /* storj.io/common encryption.PadReader: p = 4 +
  * (bs - (len+4) % bs) % bs pad bytes, every pad byte = byte(p), the last 4

@@ -56,6 +56,11 @@ def lib():
         L.or_baseline_rebuild_segment.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int,
                                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u8p),
                                                   ctypes.c_size_t, u8p, ctypes.c_int]
+        L.or_fast_encode_segment.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, u8p,
+                                             ctypes.c_size_t, u8p, ctypes.c_int]
+        L.or_fast_rebuild_segment.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p,
+                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u8p),
+                                              ctypes.c_size_t, u8p, ctypes.c_int]
         L.or_pad.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t]
         L.or_pad.restype = ctypes.c_size_t
         L.or_get_simd.restype = ctypes.c_int
@@ -168,6 +173,29 @@ class FEC:
         out = np.empty(stripes * self.k * ess, dtype=np.uint8)
         rc = lib().or_baseline_rebuild_segment(self.k, self.n, ess, _p(self.enc), ns, carr, parr, stripes,
                                                _p(out), threads)
+        if rc:
+            raise _err(rc)
+        return out
+
+    # the optimised CPU variant (all rows per block of stripes; one inversion per share set)
+    def fast_encode_segment(self, seg: np.ndarray, ess: int, threads: int = 1) -> np.ndarray:
+        seg = np.ascontiguousarray(seg, dtype=np.uint8)
+        stripes = len(seg) // (self.k * ess)
+        assert stripes * self.k * ess == len(seg)
+        pieces = np.empty((self.n, stripes * ess), dtype=np.uint8)
+        lib().or_fast_encode_segment(self.k, self.n, ess, _p(self.enc), _p(seg), stripes, _p(pieces), threads)
+        return pieces
+
+    def fast_rebuild_segment(self, nums, pieces, ess: int, threads: int = 1) -> np.ndarray:
+        """rebuild from exactly k pieces"""
+        nums = list(nums)
+        assert len(nums) == self.k
+        stripes = len(pieces[0]) // ess
+        keep = [np.ascontiguousarray(p, dtype=np.uint8) for p in pieces]
+        carr = (ctypes.c_int * self.k)(*nums)
+        parr = (ctypes.POINTER(ctypes.c_uint8) * self.k)(*[_p(p) for p in keep])
+        out = np.empty(stripes * self.k * ess, dtype=np.uint8)
+        rc = lib().or_fast_rebuild_segment(self.k, self.n, ess, _p(self.enc), carr, parr, stripes, _p(out), threads)
         if rc:
             raise _err(rc)
         return out

@@ -183,12 +183,17 @@ static void adjacent_stages(void) {
 }
 
 int main(void) {
+    setvbuf(stdout, NULL, _IONBF, 0); /* progress survives an abort */
     ec_ctx *bad = NULL;
     CHECK(ec_create(0, 4, 256, &bad) == EC_ERR_PARAMS, "k = 0");
     CHECK(ec_create(5, 4, 256, &bad) == EC_ERR_PARAMS, "k > n");
     CHECK(ec_device_count() >= 1, "no device");
     const int cfg[][3] = {{2, 4, 1024}, {4, 10, 256}, {29, 80, 256}, {20, 60, 4096}, {3, 7, 100}, {10, 20, 64}};
-    for (size_t i = 0; i < sizeof cfg / sizeof cfg[0]; i++) scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2]);
+    for (size_t i = 0; i < sizeof cfg / sizeof cfg[0]; i++) {
+        printf("RS(%d,%d) ess %d\n", cfg[i][0], cfg[i][1], cfg[i][2]);
+        scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2]);
+    }
+    printf("adjacent stages\n");
     adjacent_stages();
     printf("%s: %d failures\n", failures ? "FAIL" : "ok", failures);
     return failures ? 1 : 0;

@@ -489,3 +489,59 @@ def test_decode_bad_pieces_over_long_runs(oracle, extra, bad, scatter):
         assert np.array_equal(s.data, allsh[s.number])
     # the same inputs through the oracle's per-column decode
     assert np.array_equal(oracle.FEC(k, n).decode(nums, [r.copy() for r in recv]), data)
+
+
+# ---- compile-time-G encoders for any (k, n) (rs_encoder.hpp) ----------------
+
+def _kernel_name(sch):
+    return sch._lib.ec_encode_kernel_name(sch._ctx).decode()
+
+
+@pytest.mark.parametrize("k,n", [(20, 50), (30, 60), (50, 80), (2, 4)])
+def test_reference_bench_configs_use_library_encoders(oracle, k, n):
+    """BenchmarkReedSolomonErasureScheme's configurations
+    (private/eestream/rs_test.go:553-634) are built into the library: 8 MiB of
+    stripes, all pieces and parity only, bit-exact vs the oracle.  RS(50,80)
+    stages its 50 inputs in two chunks (rs_encoder.hpp kMaxChunk)."""
+    ess = 256
+    stripes = (8 << 20) // (k * ess)
+    sch = scheme(k, n, ess)
+    assert _kernel_name(sch) == "special"
+    rng = np.random.default_rng(k * 131 + n)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    assert np.array_equal(gpu_encode(sch, seg).cpu().numpy()[0], ref)
+    assert np.array_equal(gpu_encode(sch, seg, parity_only=True).cpu().numpy()[0], ref[k:])
+
+
+@pytest.mark.parametrize("k,n,stripes", [(5, 9, 33), (37, 50, 17), (10, 20, 1025)])
+def test_run_time_compiled_encoder(oracle, k, n, stripes):
+    """(k, n) without a library-built encoder: compiled by hiprtc from the
+    same header text (waited for here), then bit-exact vs the oracle, for all
+    pieces and parity only, batched over 3 segments.  RS(37,50) needs two
+    input chunks.  Before it is ready the same calls run the runtime-matrix
+    kernel (test_encode_rebuild_vs_oracle covers that path)."""
+    ess = 256
+    sch = scheme(k, n, ess)
+    assert sch._lib.ec_prepare_encoder(sch._ctx, 1) == 1
+    assert _kernel_name(sch) == "special-jit"
+    rng = np.random.default_rng(k * 7 + n)
+    nseg = 3
+    seg = rng.integers(0, 256, nseg * stripes * k * ess, dtype=np.uint8)
+    f = oracle.FEC(k, n)
+    refs = [f.encode_segment(seg[i * stripes * k * ess:(i + 1) * stripes * k * ess], ess, threads=8)
+            for i in range(nseg)]
+    got = gpu_encode(sch, seg, nseg=nseg).cpu().numpy()
+    par = gpu_encode(sch, seg, nseg=nseg, parity_only=True).cpu().numpy()
+    for i in range(nseg):
+        assert np.array_equal(got[i], refs[i]), i
+        assert np.array_equal(par[i], refs[i][k:]), i
+
+
+def test_prepare_encoder_reports_limits():
+    # n - k > 96 parity rows: outside the compile-time encoder (runtime-matrix kernel)
+    sch = scheme(7, 200, 256)
+    assert sch._lib.ec_prepare_encoder(sch._ctx, 0) == 0
+    assert _kernel_name(sch) == "generic"
+    s2 = scheme(29, 80, 256)
+    assert s2._lib.ec_prepare_encoder(s2._ctx, 0) == 1

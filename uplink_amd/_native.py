@@ -83,6 +83,7 @@ SIGNATURES = {
     "ec_device_count": (ctypes.c_int, []),
     "ec_set_device": (ctypes.c_int, [ctypes.c_int]),
     "ec_encode_kernel_name": (ctypes.c_char_p, [vp]),
+    "ec_prepare_encoder": (ctypes.c_int, [vp, ctypes.c_int]),
 }
 
 _lib = None

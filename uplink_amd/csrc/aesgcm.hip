@@ -87,26 +87,14 @@ __device__ constexpr uint32_t kRem4[16] = {0x0000u << 16, 0x1C20u << 16, 0x3840u
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
 
-// T-table layout.  kCopies = 0: T0..T3 once each (4 KB; random lanes collide
-// on LDS banks).  kCopies = C > 0: T0 alone, replicated C times with copy c of
-// entry x at word x*C + c, lane l reading copy l % C, so lanes read distinct
-// banks (C = 64) or at most two share one (C = 32); T1..T3 are rotations.
-// experiment switch (tools/exp/gcm_var.cpp): 1 = skip the GHASH Horner multiplies,
-// 2 = skip the AES rounds; results are then wrong
-#ifndef UPLINK_GCM_EXP
-#define UPLINK_GCM_EXP 0
-#endif
-#ifndef UPLINK_GCM_COPIES
-#define UPLINK_GCM_COPIES 32
-#endif
-#ifndef UPLINK_GCM_TABLES
-#define UPLINK_GCM_TABLES 1
-#endif
-constexpr int kCopies = UPLINK_GCM_COPIES;
-constexpr int kTables = UPLINK_GCM_TABLES;  // 1: T0 only, T1..T3 by rotation; 4: all four stored
+// T-table layout: T0 alone, replicated kCopies times with copy c of entry x
+// at word x*kCopies + c; lane l reads copy l % kCopies, so at most two lanes
+// share an LDS bank; T1..T3 are rotations of T0 (DESIGN.md §4c has the
+// measured alternatives).
+constexpr int kCopies = 32;
 
 struct Lds {
-    uint32_t t[kCopies ? kTables * 256 * kCopies : 4 * 256];
+    uint32_t t[256 * kCopies];
     uint32_t rem[16];
     uint32_t htab[64][16][4];    // H^1..H^64
 };
@@ -114,19 +102,13 @@ struct Lds {
 // Tk[x] for this lane
 template <int k>
 __device__ __forceinline__ uint32_t T(const Lds &L, uint32_t x, uint32_t copy) {
-    if constexpr (kCopies == 0) {
-        return L.t[k * 256 + x];
-    } else if constexpr (kTables == 4) {
-        return L.t[(k * 256 + x) * kCopies + copy];
-    } else {
-        const uint32_t v = L.t[x * kCopies + copy];
-        return k ? __builtin_amdgcn_alignbit(v, v, 8 * k) : v;
-    }
+    const uint32_t v = L.t[x * kCopies + copy];
+    return k ? __builtin_amdgcn_alignbit(v, v, 8 * k) : v;
 }
 
 // AES-256 of the big-endian words s[4] with round keys rk (SGPRs), T-tables in LDS
 __device__ __forceinline__ void aes_encrypt(uint32_t (&s)[4], const uint32_t *__restrict__ rk, const Lds &L) {
-    const uint32_t cp = kCopies ? threadIdx.x % (kCopies ? kCopies : 1) : 0;
+    const uint32_t cp = threadIdx.x % kCopies;
     uint32_t a = s[0] ^ rk[0], b = s[1] ^ rk[1], c = s[2] ^ rk[2], d = s[3] ^ rk[3];
 #pragma unroll
     for (int r = 1; r < 14; r++) {
@@ -176,26 +158,13 @@ __device__ __forceinline__ void load_tail(const uint8_t *p, uint32_t n, uint32_t
     for (uint32_t i = 0; i < n; i++) w[i >> 2] |= (uint32_t)p[i] << (24 - 8 * (i & 3));
 }
 
-#ifndef UPLINK_GCM_WGS_PER_CU
-#define UPLINK_GCM_WGS_PER_CU 1
-#endif
 template <bool kOpen>
-__global__ __launch_bounds__(256, UPLINK_GCM_WGS_PER_CU) void gcm_blocks(GcmBatch a, uint32_t wgs_per_seg) {
+__global__ __launch_bounds__(256, 1) void gcm_blocks(GcmBatch a, uint32_t wgs_per_seg) {
     __shared__ Lds L;
     const uint32_t seg = blockIdx.x / wgs_per_seg;
     const uint32_t wg = blockIdx.x % wgs_per_seg;
     const GcmSched *ks = a.sched + seg;
-    if constexpr (kCopies == 0) {
-        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-            const uint32_t t0 = kAesDev.t0[i];
-            L.t[i] = t0, L.t[256 + i] = ror32(t0, 8), L.t[512 + i] = ror32(t0, 16), L.t[768 + i] = ror32(t0, 24);
-        }
-    } else {
-        for (int i = threadIdx.x; i < kTables * 256 * kCopies; i += blockDim.x) {
-            const int e = i / (kCopies ? kCopies : 1);  // table * 256 + entry
-            L.t[i] = ror32(kAesDev.t0[e & 255], 8 * (e >> 8));
-        }
-    }
+    for (int i = threadIdx.x; i < 256 * kCopies; i += blockDim.x) L.t[i] = kAesDev.t0[i / kCopies];
     if (threadIdx.x < 16) L.rem[threadIdx.x] = kRem4[threadIdx.x];
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(&ks->htab[0][0][0]);
@@ -242,7 +211,7 @@ __global__ __launch_bounds__(256, UPLINK_GCM_WGS_PER_CU) void gcm_blocks(GcmBatc
             // every lane runs the AES (no divergent second pass): data lanes on their counter block,
             // padding lanes on J0 (the tag mask), the length-block lane on a value it ignores
             uint32_t ks4[4] = {j0w0, j0w1, j0w2, is_data ? 2 + sidx : 1};
-            if (UPLINK_GCM_EXP != 2) aes_encrypt(ks4, rk, L);
+            aes_encrypt(ks4, rk, L);
             uint32_t y[4] = {0, 0, 0, 0};
             if (is_data) {
                 const uint32_t n = (sidx + 1 == nsub && tail) ? tail : 16;
@@ -282,8 +251,7 @@ __global__ __launch_bounds__(256, UPLINK_GCM_WGS_PER_CU) void gcm_blocks(GcmBatc
             // Horner step with H^64
             if (j) {
                 uint32_t m[4];
-                if (UPLINK_GCM_EXP != 1) gf_mul(m, acc, L.htab[63], L.rem);
-                else m[0] = acc[0], m[1] = acc[1], m[2] = acc[2], m[3] = acc[3];
+                gf_mul(m, acc, L.htab[63], L.rem);
 #pragma unroll
                 for (int q = 0; q < 4; q++) acc[q] = m[q] ^ y[q];
             } else {

@@ -102,13 +102,9 @@ struct B3Pair {
     uint64_t split;
 };
 
-// chunks per lane.  2 folds the first tree level in registers at full lane
-// utilisation (the LDS fold then starts from 256 level-1 nodes), but halves
-// the waves in flight: 72.5 against 67.9 us per segment, so 1.
-#ifndef UPLINK_B3_PAIR
-#define UPLINK_B3_PAIR 1
-#endif
-constexpr int kPerLane = UPLINK_B3_PAIR;
+// chunks per lane (two per lane, folding the first tree level in registers,
+// halved the waves in flight and measured slower: DESIGN.md §4b)
+constexpr int kPerLane = 1;
 constexpr int kGroupChunks = kGroup * kPerLane;  // chunks per workgroup
 
 // CV of chunk c of a piece (ROOT on its last block when `root`)
@@ -118,7 +114,7 @@ __device__ __forceinline__ void chunk_cv(const B3View &v, const uint8_t *pb, uin
     const uint64_t clen = v.piece_len - t0 < 1024 ? v.piece_len - t0 : 1024;  // 0 only for an empty piece
 #pragma unroll
     for (int i = 0; i < 8; i++) h[i] = kIV[i];
-    if (UPLINK_B3_LINES && kFast && clen == 1024 && v.run_shift >= 7) {
+    if (kFast && clen == 1024 && v.run_shift >= 7) {
         full_chunk_lines(v, pb, t0, c, kChunkEnd | (root ? kRoot : 0), h);
         return;
     }

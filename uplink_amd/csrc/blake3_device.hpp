@@ -9,13 +9,7 @@ namespace uplink_ec {
 namespace b3 {
 
 constexpr uint32_t kChunkStart = 1, kChunkEnd = 2, kParent = 4, kRoot = 8;
-#ifndef UPLINK_B3_GROUP
-#define UPLINK_B3_GROUP 256
-#endif
-#ifndef UPLINK_B3_LINES
-#define UPLINK_B3_LINES 1
-#endif
-constexpr int kGroup = UPLINK_B3_GROUP;  // chunks (or nodes) folded per workgroup (variants: tools/exp/b3_var.cpp)
+constexpr int kGroup = 256;  // chunks (or nodes) folded per workgroup (256 measured best)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ constexpr uint32_t kIV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,

@@ -26,24 +26,44 @@ using namespace uplink_ec;
 
 namespace {
 
-struct DecodePlan {
-    std::vector<int> ids;      // chosen share numbers, position i = infectious row i
-    std::vector<int> missing;  // positions i (== data number) rebuilt
-    uint8_t *d_coef = nullptr; // [c][r] = Dinv[missing[r]][c], ld = coef_ld
-    int coef_ld = 0;
-    uint64_t *d_tgt = nullptr; // jump-table leaf addresses of d_coef (launch_jt_targets)
-    ~DecodePlan() {
-        // hipFree synchronises with outstanding device work before releasing
+// A runtime matrix M (rows x nin) uploaded for the generic kernels: the
+// coefficients coef[j][r] = M[r][j] and, for the bit-sliced kernel, the
+// jump-table leaf addresses of every block of up to kMaxOps rows
+// (launch_jt_targets).  Plans are built once -- synchronously, on the
+// context's own setup stream -- and reused by every launch of that matrix, so
+// no launch allocates memory or prepares tables in stream order.
+struct MatPlan {
+    std::vector<int> key;          // what the matrix is (decode: chosen share ids; see plan keys below)
+    std::vector<int> missing;      // decode plans: the data positions rebuilt, in row order
+    int rows = 0, nin = 0, coef_ld = 0;
+    uint8_t *d_coef = nullptr;     // [j][r], ld = coef_ld
+    std::vector<uint64_t *> d_tgt; // leaf addresses per block of kMaxOps rows
+    ~MatPlan() {
         if (d_coef) (void)hipFree(d_coef);
-        if (d_tgt) (void)hipFree(d_tgt);
+        for (uint64_t *t : d_tgt)
+            if (t) (void)hipFree(t);
     }
 };
-using PlanPtr = std::shared_ptr<DecodePlan>;
+using PlanPtr = std::shared_ptr<MatPlan>;
 
 struct Workspace {
     uint8_t *d_buf = nullptr;
     size_t cap = 0;
     hipStream_t stream = nullptr;
+};
+
+// Every export that takes a context runs on the context's device and
+// restores the caller's current device on return (a Go caller's goroutine
+// may move between OS threads, each with its own current device).
+struct DeviceGuard {
+    int prev = -1;
+    bool switched = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) switched = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (switched) (void)hipSetDevice(prev);
+    }
 };
 
 }  // namespace
@@ -61,12 +81,15 @@ struct ec_ctx {
     std::mutex pipe_mu;  // one host pipeline at a time per context
     HostPipe pipe;
     std::vector<uint8_t> G;        // n x k
-    uint8_t *d_coef_all = nullptr; // [j][i] = G[i][j], ld = ld_all
-    int ld_all = 0;
+    hipStream_t setup = nullptr;   // plan uploads (synchronous, never a caller's stream)
+    std::mutex setup_mu;
     std::mutex mu;
-    std::list<PlanPtr> plans;      // MRU first
+    std::list<PlanPtr> plans;      // decode / re-encode plans, MRU first
+    PlanPtr enc_parity;            // rows k..n-1 of G
+    std::vector<PlanPtr> enc_row;  // row num of G (EncodeSingle)
     std::vector<Workspace *> free_ws;
     std::vector<std::unique_ptr<Workspace>> all_ws;
+    uint32_t *d_chk = nullptr;     // checked build: the kernels' violation word
 };
 
 namespace {
@@ -128,23 +151,161 @@ void fill_geometry(RsArgs &a, int ess, int64_t nstripes, int64_t nseg) {
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
-// Launch a matrix product described by `a` (rows a.nout, possibly > kMaxOps:
-// split into several launches; copies happen in the first one only).
-int run_matmul(RsArgs a, int64_t nseg, bool bitsliced, hipStream_t s) {
-    const int total_rows = a.nout;
-    int64_t out_off_all[256];
-    for (int r = 0; r < total_rows; r++) out_off_all[r] = a.out_off[r];
-    const uint8_t *coef0 = a.coef;
-    if (total_rows > kMaxOps) a.jt_tgt = nullptr;  // a prepared table covers one launch of all rows
-    int done = 0;
-    bool first = true;
+// The byte ranges a launch may touch, from its geometry (RsArgs::chk_*).
+void set_extents(RsArgs &a, int64_t nseg, uint32_t *chk) {
+    a.chk_flag = chk;
+    int64_t ilo = INT64_MAX, ihi = 0, olo = INT64_MAX, ohi = 0;
+    for (int j = 0; j < a.nin; j++) {
+        ilo = std::min(ilo, a.in_off[j]);
+        ihi = std::max(ihi, a.in_off[j]);
+        if (a.copy_off[j] >= 0) olo = std::min(olo, a.copy_off[j]), ohi = std::max(ohi, a.copy_off[j]);
+    }
+    for (int r = 0; r < a.nout; r++) olo = std::min(olo, a.out_off[r]), ohi = std::max(ohi, a.out_off[r]);
+    const int64_t last = nseg > 0 && a.nstripes > 0;
+    a.chk_in_lo = a.in_base + (ilo == INT64_MAX ? 0 : ilo);
+    a.chk_in_hi = a.in_base + ihi + last * ((nseg - 1) * a.in_seg_stride + (a.nstripes - 1) * a.in_stripe_stride + a.ess);
+    a.chk_out_lo = a.out_base + (olo == INT64_MAX ? 0 : olo);
+    a.chk_out_hi =
+        a.out_base + ohi + last * ((nseg - 1) * a.out_seg_stride + (a.nstripes - 1) * a.out_stripe_stride + a.ess);
+}
+
+// Upload M (rows x nin, row-major) and its leaf-address tables; synchronous.
+int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int nin, PlanPtr *out) {
+    PlanPtr p = std::make_shared<MatPlan>();
+    p->key = std::move(key);
+    p->rows = rows;
+    p->nin = nin;
+    p->coef_ld = round16(std::max(rows, 1));
+    std::vector<uint8_t> coef((size_t)nin * p->coef_ld + kCoefPad, 0);
+    for (int r = 0; r < rows; r++)
+        for (int j = 0; j < nin; j++) coef[(size_t)j * p->coef_ld + r] = M[(size_t)r * nin + j];
+    std::lock_guard<std::mutex> g(c->setup_mu);
+    HIP_TRY(hipMalloc(&p->d_coef, coef.size()));
+    HIP_TRY(hipMemcpyAsync(p->d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice, c->setup));
+    for (int r0 = 0; r0 < std::max(rows, 1); r0 += kMaxOps) {
+        RsArgs t{};
+        t.coef = p->d_coef + r0;
+        t.coef_ld = p->coef_ld;
+        t.nin = nin;
+        t.nout = std::min(kMaxOps, rows - r0);
+        uint64_t *tgt = nullptr;
+        HIP_TRY(hipMalloc(&tgt, jt_targets_bytes(t)));
+        p->d_tgt.push_back(tgt);
+        HIP_TRY(launch_jt_targets(t, tgt, c->setup));
+    }
+    HIP_TRY(hipStreamSynchronize(c->setup));  // `coef` (pageable) is consumed before it goes away
+    *out = p;
+    return EC_OK;
+}
+
+// Cached plan for `key`, built from make_matrix() on a miss.
+template <typename F>
+int cached_plan(ec_ctx *c, const std::vector<int> &key, F &&make_matrix, PlanPtr *out) {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        for (auto it = c->plans.begin(); it != c->plans.end(); ++it) {
+            if ((*it)->key == key) {
+                c->plans.splice(c->plans.begin(), c->plans, it);
+                *out = c->plans.front();
+                return EC_OK;
+            }
+        }
+    }
+    std::vector<uint8_t> M;
+    std::vector<int> missing;
+    int rows = 0;
+    int rc = make_matrix(M, rows, missing);
+    if (rc) return rc;
+    PlanPtr p;
+    rc = build_plan(c, key, M.data(), rows, c->k, &p);
+    if (rc) return rc;
+    p->missing = std::move(missing);
+    std::vector<PlanPtr> evicted;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->plans.push_front(p);
+        while (c->plans.size() > kMaxPlans) {
+            evicted.push_back(c->plans.back());
+            c->plans.pop_back();
+        }
+    }
+    // an evicted plan may still be read by launches in flight on callers' streams
+    if (!evicted.empty()) (void)hipDeviceSynchronize();
+    *out = p;
+    return EC_OK;
+}
+
+// Plan of the parity rows k..n-1 (encode for (k, n) without a compile-time kernel)
+int parity_plan(ec_ctx *c, PlanPtr *out) {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (c->enc_parity) {
+            *out = c->enc_parity;
+            return EC_OK;
+        }
+    }
+    PlanPtr p;
+    int rc = build_plan(c, {-3}, c->G.data() + (size_t)c->k * c->k, c->n - c->k, c->k, &p);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->enc_parity) c->enc_parity = p;
+    *out = c->enc_parity;
+    return EC_OK;
+}
+
+// Plan of row `num` of G (ErasureScheme.EncodeSingle)
+int row_plan(ec_ctx *c, int num, PlanPtr *out) {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (c->enc_row[num]) {
+            *out = c->enc_row[num];
+            return EC_OK;
+        }
+    }
+    PlanPtr p;
+    int rc = build_plan(c, {-4, num}, c->G.data() + (size_t)num * c->k, 1, c->k, &p);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->enc_row[num]) c->enc_row[num] = p;
+    *out = c->enc_row[num];
+    return EC_OK;
+}
+
+// Checked build: wait for the launch just made and fail if a kernel skipped an
+// access outside the launch's declared ranges (rs_tile.hpp in_range).
+int after_launch(uint32_t *chk, hipStream_t s) {
+#ifdef UPLINK_EC_CHECKED
+    uint32_t site = 0;
+    HIP_TRY(hipMemcpyAsync(&site, chk, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (site) {
+        fprintf(stderr, "uplink_ec checked: a kernel addressed memory outside its launch's ranges (site %u)\n", site);
+        return EC_ERR_INVALID_ARG;
+    }
+#else
+    (void)chk, (void)s;
+#endif
+    return EC_OK;
+}
+
+// Launch the product described by `a` with the rows of `plan` (out_off gives
+// every row's offset; more than kMaxOps rows go in several launches, copies
+// in the first one only).
+int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, const MatPlan &plan, int64_t nseg, bool bitsliced,
+               hipStream_t s) {
+    const int total_rows = plan.rows;
+    int done = 0, blk = 0;
     do {
         const int rows = std::min(kMaxOps, total_rows - done);
         a.nout = rows;
-        for (int r = 0; r < rows; r++) a.out_off[r] = out_off_all[done + r];
-        a.coef = coef0 + done;
-        if (!first)
+        a.nin = plan.nin;
+        a.coef = plan.d_coef + done;
+        a.coef_ld = plan.coef_ld;
+        a.jt_tgt = bitsliced ? plan.d_tgt[blk] : nullptr;
+        for (int r = 0; r < rows; r++) a.out_off[r] = out_off[done + r];
+        if (done > 0)
             for (int j = 0; j < a.nin; j++) a.copy_off[j] = -1;
+        set_extents(a, nseg, c->d_chk);
         if (bitsliced) {
             HIP_TRY(launch_matmul_generic(a, 0, s));
         } else {
@@ -153,8 +314,9 @@ int run_matmul(RsArgs a, int64_t nseg, bool bitsliced, hipStream_t s) {
             HIP_TRY(launch_matmul_bytes(a, s));
             a.total_tiles = keep;
         }
+        if (int rc = after_launch(c->d_chk, s)) return rc;
         done += rows;
-        first = false;
+        blk++;
     } while (done < total_rows);
     return EC_OK;
 }
@@ -181,53 +343,23 @@ int choose_shares(const ec_ctx *c, int nshares, const int *nums, std::vector<int
     return EC_OK;
 }
 
-// Decode plan for the chosen ids (cached per share set).
+// Decode plan for the chosen ids (one inversion per share set).
 int get_plan(ec_ctx *c, const std::vector<int> &ids, PlanPtr *out) {
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        for (auto it = c->plans.begin(); it != c->plans.end(); ++it) {
-            if ((*it)->ids == ids) {
-                c->plans.splice(c->plans.begin(), c->plans, it);
-                *out = c->plans.front();
-                return EC_OK;
-            }
+    return cached_plan(c, ids, [&](std::vector<uint8_t> &M, int &rows, std::vector<int> &missing) {
+        const int k = c->k;
+        std::vector<uint8_t> m((size_t)k * k, 0);
+        for (int i = 0; i < k; i++) {
+            if (ids[i] < k) m[(size_t)i * k + i] = 1;
+            else memcpy(&m[(size_t)i * k], &c->G[(size_t)ids[i] * k], k);
         }
-    }
-    const int k = c->k;
-    std::vector<uint8_t> m((size_t)k * k, 0);
-    for (int i = 0; i < k; i++) {
-        if (ids[i] < k) m[(size_t)i * k + i] = 1;
-        else memcpy(&m[(size_t)i * k], &c->G[(size_t)ids[i] * k], k);
-    }
-    if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
-    PlanPtr p = std::make_shared<DecodePlan>();
-    p->ids = ids;
-    for (int i = 0; i < k; i++)
-        if (ids[i] >= k) p->missing.push_back(i);
-    const int R = (int)p->missing.size();
-    p->coef_ld = round16(std::max(R, 1));
-    std::vector<uint8_t> coef((size_t)k * p->coef_ld + kCoefPad, 0);
-    for (int r = 0; r < R; r++)
-        for (int col = 0; col < k; col++) coef[(size_t)col * p->coef_ld + r] = m[(size_t)p->missing[r] * k + col];
-    HIP_TRY(hipMalloc(&p->d_coef, coef.size()));
-    HIP_TRY(hipMemcpy(p->d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice));
-    if (R > 0 && R <= kMaxOps) {  // the generic kernel's leaf addresses, made once per plan
-        RsArgs t{};
-        t.coef = p->d_coef;
-        t.coef_ld = p->coef_ld;
-        t.nin = k;
-        t.nout = R;
-        HIP_TRY(hipMalloc(&p->d_tgt, jt_targets_bytes(t)));
-        HIP_TRY(launch_jt_targets(t, p->d_tgt, nullptr));
-        HIP_TRY(hipStreamSynchronize(nullptr));
-    }
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        c->plans.push_front(p);
-        while (c->plans.size() > kMaxPlans) c->plans.pop_back();
-    }
-    *out = p;
-    return EC_OK;
+        if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
+        for (int i = 0; i < k; i++)
+            if (ids[i] >= k) missing.push_back(i);
+        rows = (int)missing.size();
+        M.assign((size_t)std::max(rows, 1) * k, 0);
+        for (int r = 0; r < rows; r++) memcpy(&M[(size_t)r * k], &m[(size_t)missing[r] * k], k);
+        return EC_OK;
+    }, out);
 }
 
 // Core rebuild: device pointers of the nshares pieces, nstripes stripes of
@@ -237,25 +369,20 @@ int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const
     std::vector<int> order, ids;
     int rc = choose_shares(c, nshares, nums, order, ids);
     if (rc) return rc;
+    const int k = c->k;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
     PlanPtr plan;
     rc = get_plan(c, ids, &plan);
     if (rc) return rc;
-    const int k = c->k;
-    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
     RsArgs a{};
     const uint8_t *base = pieces[order[0]];
     for (int i = 0; i < k; i++) base = std::min(base, pieces[order[i]]);
     a.in_base = base;
     a.out_base = out;
-    a.coef = plan->d_coef;
-    a.coef_ld = plan->coef_ld;
-    a.jt_tgt = plan->d_tgt;
     a.in_stripe_stride = ess;
     a.out_stripe_stride = (int64_t)k * ess;
     a.in_seg_stride = piece_seg_stride;
     a.out_seg_stride = out_seg_stride;
-    a.nin = k;
-    a.nout = (int)plan->missing.size();
     bool bits = (ess % 16) == 0 && aligned16(out);
     for (int i = 0; i < k; i++) {
         const uint8_t *p = pieces[order[i]];
@@ -263,10 +390,11 @@ int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const
         a.copy_off[i] = ids[i] < k ? (int64_t)ids[i] * ess : -1;
         bits = bits && aligned16(p);
     }
-    for (int r = 0; r < a.nout; r++) a.out_off[r] = (int64_t)plan->missing[r] * ess;
+    std::vector<int64_t> out_off(std::max<size_t>(plan->missing.size(), 1));
+    for (size_t r = 0; r < plan->missing.size(); r++) out_off[r] = (int64_t)plan->missing[r] * ess;
     fill_geometry(a, ess, nstripes, nseg);
     if (!bits) a.cps = 1;
-    return run_matmul(a, nseg, bits, s);
+    return run_matmul(c, a, out_off.data(), *plan, nseg, bits, s);
 }
 
 }  // namespace
@@ -298,29 +426,41 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     c->G.resize((size_t)n * k);
     for (int i = 0; i < n; i++)
         for (int j = 0; j < k; j++) c->G[(size_t)i * k + j] = gen_entry(k, i, j);
-    c->ld_all = round16(n);
-    std::vector<uint8_t> coef((size_t)k * c->ld_all + kCoefPad, 0);
-    for (int j = 0; j < k; j++)
-        for (int i = 0; i < n; i++) coef[(size_t)j * c->ld_all + i] = c->G[(size_t)i * k + j];
-    HIP_TRY(hipMalloc(&c->d_coef_all, coef.size()));
-    HIP_TRY(hipMemcpy(c->d_coef_all, coef.data(), coef.size(), hipMemcpyHostToDevice));
+    c->enc_row.resize(n);
+    HIP_TRY(hipStreamCreateWithFlags(&c->setup, hipStreamNonBlocking));
+    // Scratch of ec_hash_segments / ec_blake3_pieces comes from the default pool
+    // in stream order: keep the pool's memory mapped between calls instead of
+    // returning it to the driver at every synchronisation.
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, c->device) == hipSuccess && pool) {
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+#ifdef UPLINK_EC_CHECKED
+    HIP_TRY(hipMalloc(&c->d_chk, 4));
+    HIP_TRY(hipMemset(c->d_chk, 0, 4));
+#endif
     *out = c.release();
     return EC_OK;
 }
 
 void ec_destroy(ec_ctx *c) {
     if (!c) return;
+    DeviceGuard dg(c->device);
     for (int s = 0; s < HostPipe::kSlots; s++) {
         if (c->pipe.st[s]) (void)hipStreamSynchronize(c->pipe.st[s]), (void)hipStreamDestroy(c->pipe.st[s]);
         if (c->pipe.d_in[s]) (void)hipFree(c->pipe.d_in[s]);
         if (c->pipe.d_out[s]) (void)hipFree(c->pipe.d_out[s]);
     }
-    c->plans.clear();
     for (auto &w : c->all_ws) {
         if (w->stream) (void)hipStreamSynchronize(w->stream), (void)hipStreamDestroy(w->stream);
         if (w->d_buf) (void)hipFree(w->d_buf);
     }
-    if (c->d_coef_all) (void)hipFree(c->d_coef_all);
+    c->plans.clear();
+    c->enc_parity.reset();
+    c->enc_row.clear();
+    if (c->setup) (void)hipStreamSynchronize(c->setup), (void)hipStreamDestroy(c->setup);
+    if (c->d_chk) (void)hipFree(c->d_chk);
     delete c;
 }
 
@@ -368,7 +508,17 @@ int ec_format_error(const ec_ctx *c, int code, long long arg, char *buf, size_t 
 const char *ec_encode_kernel_name(const ec_ctx *c) {
     if (!c) return "";
     if (c->ess % 16) return "bytes";
-    return have_special_encoder(c->k, c->n) ? "special" : "generic";
+    if (c->n == c->k) return "copy";
+    DeviceGuard dg(c->device);
+    const EncoderKernel *e = find_encoder(c->k, c->n);
+    return e ? (e->jit ? "special-jit" : "special") : "generic";
+}
+
+int ec_prepare_encoder(const ec_ctx *c, int wait) {
+    if (!c) return EC_ERR_INVALID_ARG;
+    if (c->n == c->k || !encoder_supported(c->k, c->n)) return 0;
+    DeviceGuard dg(c->device);
+    return find_encoder(c->k, c->n, wait != 0) ? 1 : 0;
 }
 
 // Encode stripes [s0, s1) of nseg segments of nstripes stripes each: the
@@ -388,8 +538,6 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
     RsArgs a{};
     a.in_base = segs;
     a.out_base = pieces;
-    a.coef = c->d_coef_all + k;  // parity rows k..n-1
-    a.coef_ld = c->ld_all;
     a.in_stripe_stride = (int64_t)k * ess;
     a.out_stripe_stride = ess;
     a.in_seg_stride = (int64_t)nstripes * k * ess;
@@ -400,41 +548,33 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
         a.in_off[j] = (int64_t)j * ess;
         a.copy_off[j] = parity_only ? -1 : (int64_t)j * piece_len;
     }
-    int64_t out_off[256];
+    std::vector<int64_t> out_off(std::max(n - k, 1));
     for (int r = 0; r < n - k; r++) out_off[r] = (int64_t)(parity_only ? r : k + r) * piece_len;
     for (int r = 0; r < std::min(n - k, kMaxOps); r++) a.out_off[r] = out_off[r];
     fill_geometry(a, ess, (int64_t)(s1 - s0), (int64_t)nseg);
     const bool bits = (ess % 16) == 0 && aligned16(segs) && aligned16(pieces);
-    if (bits && have_special_encoder(k, n)) {
-        HIP_TRY(launch_encode_special(k, n, a, 0, s));
-        return EC_OK;
+    if (n == k) {  // replication of the data only: copies, no parity rows
+        if (parity_only) return EC_OK;
+    } else if (bits) {
+        const EncoderKernel *ek = find_encoder(c->k, c->n);
+        if (ek) {
+            a.coef = nullptr;
+            set_extents(a, (int64_t)nseg, c->d_chk);
+            HIP_TRY(launch_encode_special(*ek, a, 0, s));
+            return after_launch(c->d_chk, s);
+        }
     }
     if (!bits) a.cps = 1;
-    // rows beyond kMaxOps are handled by run_matmul's split
-    if (n - k > kMaxOps) {
-        // run_matmul reads a.out_off for all rows: pass through a widened copy
-        RsArgs b = a;
-        int done = 0;
-        bool first = true;
-        while (done < n - k) {
-            const int rows = std::min(kMaxOps, n - k - done);
-            b.nout = rows;
-            b.coef = c->d_coef_all + k + done;
-            for (int r = 0; r < rows; r++) b.out_off[r] = out_off[done + r];
-            if (!first)
-                for (int j = 0; j < k; j++) b.copy_off[j] = -1;
-            int rc = run_matmul(b, (int64_t)nseg, bits, s);
-            if (rc) return rc;
-            done += rows;
-            first = false;
-        }
-        return EC_OK;
-    }
-    return run_matmul(a, (int64_t)nseg, bits, s);
+    PlanPtr plan;
+    int rc = parity_plan(c, &plan);
+    if (rc) return rc;
+    return run_matmul(c, a, out_off.data(), *plan, (int64_t)nseg, bits, s);
 }
 
 int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
                        int flags, ec_stream stream) {
+    if (!cc) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(cc->device);
     return encode_range(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, 0, nstripes, pieces, flags,
                         (hipStream_t)stream);
 }
@@ -446,6 +586,7 @@ int ec_rebuild_segments_batched(const ec_ctx *cc, int nshares, const int *nums, 
     if (!c || !nums || !pieces || !out) return EC_ERR_INVALID_ARG;
     if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
     if (nstripes == 0 || nseg == 0) return EC_OK;
+    DeviceGuard dg(c->device);
     return rebuild_device(c, nshares, nums, pieces, c->ess, (int64_t)nstripes, (int64_t)nseg, piece_seg_stride,
                           out_seg_stride, out, (hipStream_t)stream);
 }
@@ -497,27 +638,26 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
     if (bs == 0) return EC_OK;
     if (!in || !out) return EC_ERR_INVALID_ARG;
     if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    DeviceGuard dg(c->device);
+    PlanPtr plan;
+    int rc = row_plan(c, num, &plan);
+    if (rc) return rc;
     Workspace *w = acquire_ws(c, in_len + bs + 64);
     if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
     const size_t out_at = (in_len + 15) & ~(size_t)15;
-    int rc = EC_OK;
     do {
         if (hipMemcpyAsync(w->d_buf, in, in_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         RsArgs a{};
         a.in_base = w->d_buf;
         a.out_base = w->d_buf + out_at;
-        a.coef = c->d_coef_all + num;
-        a.coef_ld = c->ld_all;
         a.in_stripe_stride = (int64_t)in_len;
         a.out_stripe_stride = (int64_t)bs;
-        a.nin = c->k;
-        a.nout = 1;
         for (int j = 0; j < c->k; j++) { a.in_off[j] = (int64_t)j * bs; a.copy_off[j] = -1; }
-        a.out_off[0] = 0;
+        const int64_t out_off = 0;
         fill_geometry(a, (int)bs, 1, 1);
         const bool bits = (bs % 16) == 0;
         if (!bits) a.cps = 1;
-        rc = run_matmul(a, 1, bits, w->stream);
+        rc = run_matmul(c, a, &out_off, *plan, 1, bits, w->stream);
         if (rc) break;
         if (hipMemcpyAsync(out, w->d_buf + out_at, bs, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
@@ -533,28 +673,28 @@ int ec_encode(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out) 
     const size_t bs = in_len / c->k;
     if (bs == 0) return EC_OK;
     if (!in || !out) return EC_ERR_INVALID_ARG;
+    if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    DeviceGuard dg(c->device);
+    PlanPtr plan;
+    int rc = parity_plan(c, &plan);
+    if (rc) return rc;
     const size_t out_at = (in_len + 15) & ~(size_t)15;
     Workspace *w = acquire_ws(c, out_at + bs * c->n + 64);
     if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
-    int rc = EC_OK;
     do {
         if (hipMemcpyAsync(w->d_buf, in, in_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         RsArgs a{};
         a.in_base = w->d_buf;
         a.out_base = w->d_buf + out_at;
-        a.coef = c->d_coef_all + c->k;
-        a.coef_ld = c->ld_all;
         a.in_stripe_stride = (int64_t)in_len;
         a.out_stripe_stride = (int64_t)bs;
-        a.nin = c->k;
-        a.nout = c->n - c->k;
         for (int j = 0; j < c->k; j++) { a.in_off[j] = (int64_t)j * bs; a.copy_off[j] = (int64_t)j * bs; }
-        for (int r = 0; r < std::min(a.nout, kMaxOps); r++) a.out_off[r] = (int64_t)(c->k + r) * bs;
+        std::vector<int64_t> out_off(std::max(c->n - c->k, 1));
+        for (int r = 0; r < c->n - c->k; r++) out_off[r] = (int64_t)(c->k + r) * bs;
         fill_geometry(a, (int)bs, 1, 1);
         const bool bits = (bs % 16) == 0;
         if (!bits) a.cps = 1;
-        if (a.nout > kMaxOps || c->k > kMaxOps) { rc = EC_ERR_UNSUPPORTED; break; }
-        rc = run_matmul(a, 1, bits, w->stream);
+        rc = run_matmul(c, a, out_off.data(), *plan, 1, bits, w->stream);
         if (rc) break;
         if (hipMemcpyAsync(out, w->d_buf + out_at, bs * c->n, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
@@ -583,6 +723,7 @@ int ec_rebuild(const ec_ctx *cc, int nshares, int *nums, const uint8_t **shares,
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
     if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+    DeviceGuard dg(c->device);
     sort_shares_inplace(nshares, nums, shares);
     if (share_len == 0) return EC_OK;
     if (!out) return EC_ERR_INVALID_ARG;
@@ -674,6 +815,7 @@ static int encode_host(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstri
                        uint8_t *hashes, int flags) {
     if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
     if (nseg == 0 || nstripes == 0) return EC_OK;
+    DeviceGuard dg(c->device);
     const size_t ess = c->ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
     const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
     const int rows = parity_only ? c->n - c->k : c->n;
@@ -750,6 +892,7 @@ int ec_hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity
                      uint8_t *hashes, ec_stream stream) {
     if (!c || !segs || !hashes || (c->n > c->k && !parity)) return EC_ERR_INVALID_ARG;
     if (nseg == 0) return EC_OK;
+    DeviceGuard dg(c->device);
     hipStream_t st = (hipStream_t)stream;
     void *ws = nullptr;
     HIP_TRY(hipMallocAsync(&ws, b3_segment_ws_bytes(c, nseg, nstripes), st));
@@ -801,6 +944,7 @@ int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, con
     if (!c || !nums || !pieces || !out) return EC_ERR_INVALID_ARG;
     if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
     if (nseg == 0 || nstripes == 0) return EC_OK;
+    DeviceGuard dg(c->device);
     std::vector<int> order, ids;
     int rc = choose_shares(c, nshares, nums, order, ids);
     if (rc) return rc;
@@ -877,44 +1021,42 @@ int ec_rebuild_segments_host(const ec_ctx *cc, int nshares, const int *nums, con
 static int reencode(ec_ctx *c, const uint8_t *d, size_t slot, size_t len, const int *nums, const int *basis,
                     const int *outs, int nout, uint8_t *expected, hipStream_t st) {
     const int k = c->k;
-    std::vector<uint8_t> m((size_t)k * k);
-    for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[basis[i]] * k], k);
-    if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
-    const int ld = round16(nout);
-    std::vector<uint8_t> coef((size_t)k * ld + kCoefPad, 0);
-    for (int r = 0; r < nout; r++)
-        for (int col = 0; col < k; col++) {
-            uint8_t acc = 0;
-            for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[outs[r]] * k + t], m[(size_t)t * k + col]);
-            coef[(size_t)col * ld + r] = acc;
-        }
-    uint8_t *d_coef = nullptr;
-    if (hipMallocAsync(&d_coef, coef.size(), st) != hipSuccess) return EC_ERR_DEVICE;
-    int rc = EC_OK;
-    if (hipMemcpyAsync(d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice, st) != hipSuccess) rc = EC_ERR_DEVICE;
-    if (rc == EC_OK) {
-        RsArgs a{};
-        a.in_base = d;
-        a.out_base = expected;
-        a.coef = d_coef;
-        a.coef_ld = ld;
-        a.in_stripe_stride = (int64_t)len;
-        a.out_stripe_stride = (int64_t)len;
-        a.nin = k;
-        a.nout = nout;
-        for (int j = 0; j < k; j++) {
-            a.in_off[j] = (int64_t)slot * basis[j];
-            a.copy_off[j] = -1;
-        }
-        for (int r = 0; r < nout; r++) a.out_off[r] = (int64_t)slot * r;
-        fill_geometry(a, (int)len, 1, 1);
-        const bool bits = (len % 16) == 0;
-        if (!bits) a.cps = 1;
-        rc = run_matmul(a, 1, bits, st);
+    // plan key: -1, the basis share numbers, -2, the re-encoded share numbers
+    std::vector<int> key{-1};
+    for (int i = 0; i < k; i++) key.push_back(nums[basis[i]]);
+    key.push_back(-2);
+    for (int r = 0; r < nout; r++) key.push_back(nums[outs[r]]);
+    PlanPtr plan;
+    int rc = cached_plan(c, key, [&](std::vector<uint8_t> &M, int &rows, std::vector<int> &) {
+        std::vector<uint8_t> m((size_t)k * k);
+        for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[basis[i]] * k], k);
+        if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
+        rows = nout;
+        M.assign((size_t)std::max(nout, 1) * k, 0);
+        for (int r = 0; r < nout; r++)
+            for (int col = 0; col < k; col++) {
+                uint8_t acc = 0;
+                for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[outs[r]] * k + t], m[(size_t)t * k + col]);
+                M[(size_t)r * k + col] = acc;
+            }
+        return EC_OK;
+    }, &plan);
+    if (rc) return rc;
+    RsArgs a{};
+    a.in_base = d;
+    a.out_base = expected;
+    a.in_stripe_stride = (int64_t)len;
+    a.out_stripe_stride = (int64_t)len;
+    for (int j = 0; j < k; j++) {
+        a.in_off[j] = (int64_t)slot * basis[j];
+        a.copy_off[j] = -1;
     }
-    // the coefficients must outlive the kernel: the stream-ordered free runs after it
-    (void)hipFreeAsync(d_coef, st);
-    return rc;
+    std::vector<int64_t> out_off(std::max(nout, 1));
+    for (int r = 0; r < nout; r++) out_off[r] = (int64_t)slot * r;
+    fill_geometry(a, (int)len, 1, 1);
+    const bool bits = (len % 16) == 0;
+    if (!bits) a.cps = 1;
+    return run_matmul(c, a, out_off.data(), *plan, 1, bits, st);
 }
 
 int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out) {
@@ -922,6 +1064,7 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
     if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
     const int k = c->k;
     if (nshares < k) return EC_ERR_NOT_ENOUGH_SHARES;
+    DeviceGuard dg(c->device);
     sort_shares_inplace(nshares, nums, (const uint8_t **)shares);
     if (share_len == 0) return EC_OK;
     if (!out) return EC_ERR_INVALID_ARG;
@@ -947,7 +1090,7 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
     auto bw_columns = [&](const std::vector<int64_t> &cl) -> int {  // Berlekamp-Welch on columns, in place
         if (cl.empty()) return EC_OK;
         if (hipMemcpyAsync(d + cols_at, cl.data(), cl.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-            launch_berlekamp_welch(d, slot, (const int *)(d + nums_at), k, c->n, nshares,
+            launch_berlekamp_welch(d, slot, (int64_t)share_len, (const int *)(d + nums_at), k, c->n, nshares,
                                    (const int64_t *)(d + cols_at), (int)cl.size(), (int *)(d + stat_at), st) !=
                 hipSuccess)
             return EC_ERR_DEVICE;
@@ -995,7 +1138,7 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
                     for (int i = 0; i < kSample; i++) samp[i] = cols[(size_t)i * cols.size() / kSample];
                     uint8_t *d_changed = d + samp_at + kSample * 12;
                     if (hipMemcpyAsync(d + samp_at, samp.data(), kSample * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        launch_berlekamp_welch(d, slot, (const int *)(d + nums_at), k, c->n, nshares,
+                        launch_berlekamp_welch(d, slot, (int64_t)share_len, (const int *)(d + nums_at), k, c->n, nshares,
                                                (const int64_t *)(d + samp_at), kSample, (int *)(d + samp_at + kSample * 8),
                                                st, d_changed) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
                     std::vector<int> sstat(kSample);

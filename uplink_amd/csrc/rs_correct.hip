@@ -16,7 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "gf256.hpp"
+#include "gf256_field.hpp"
 #include "rs_correct.hpp"
 
 namespace uplink_ec {
@@ -69,9 +69,9 @@ __global__ void rs_put_rows(uint8_t *shares, int64_t stride, const int *rows, in
     }
 }
 
-__global__ __launch_bounds__(64) void rs_berlekamp_welch(uint8_t *shares, int64_t stride, const int *nums, int k,
-                                                         int n, int ns, const int64_t *cols, int ncols,
-                                                         int *status, uint8_t *changed) {
+__global__ __launch_bounds__(64) void rs_berlekamp_welch(uint8_t *shares, int64_t stride, int64_t len,
+                                                         const int *nums, int k, int n, int ns, const int64_t *cols,
+                                                         int ncols, int *status, uint8_t *changed) {
     __shared__ uint8_t A[kMaxDim][kMaxDim + 1];
     __shared__ uint8_t f[kMaxDim];
     __shared__ uint8_t u[kMaxDim];
@@ -80,6 +80,10 @@ __global__ __launch_bounds__(64) void rs_berlekamp_welch(uint8_t *shares, int64_
     const int tid = threadIdx.x;
     for (int ci = blockIdx.x; ci < ncols; ci += gridDim.x) {
         const int64_t col = cols[ci];
+        if (col < 0 || col >= len) {  // host-supplied column list: never index outside the shares
+            if (tid == 0) status[ci] = -10;
+            continue;
+        }
         const int e = (ns - k) / 2;
         if (e <= 0) {
             if (tid == 0) status[ci] = -6;
@@ -190,12 +194,12 @@ hipError_t launch_flag_columns(const uint8_t *shares, int64_t stride, const uint
     return hipGetLastError();
 }
 
-hipError_t launch_berlekamp_welch(uint8_t *shares, int64_t stride, const int *nums, int k, int n, int ns,
+hipError_t launch_berlekamp_welch(uint8_t *shares, int64_t stride, int64_t len, const int *nums, int k, int n, int ns,
                                   const int64_t *cols, int ncols, int *status, hipStream_t s, uint8_t *changed) {
     int blocks = ncols < 2048 ? ncols : 2048;
     if (blocks < 1) return hipSuccess;
-    hipLaunchKernelGGL(rs_berlekamp_welch, dim3(blocks), dim3(64), 0, s, shares, stride, nums, k, n, ns, cols, ncols,
-                       status, changed);
+    hipLaunchKernelGGL(rs_berlekamp_welch, dim3(blocks), dim3(64), 0, s, shares, stride, len, nums, k, n, ns, cols,
+                       ncols, status, changed);
     return hipGetLastError();
 }
 

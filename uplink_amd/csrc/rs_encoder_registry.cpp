@@ -1,0 +1,273 @@
+// Registry of the compile-time-G encoders (rs_encoder.hpp).
+//
+// k and n arrive per segment from the satellite (metaclient/client.go:1262-1267
+// -> eestream.NewRedundancyStrategyFromProto, encode.go:69-87), so any (k, n)
+// must reach the fast encoder:
+//  * AOT: the configurations of rs_encoder_aot.def are compiled into the
+//    library (one translation unit each, rs_encode_aot.hip).
+//  * JIT: any other (k, n) inside the encoder's limits is compiled by hiprtc
+//    from the same header text (embedded at build time, rs_jit_sources.inc),
+//    in a background thread started on first request, and the code object is
+//    cached on disk.  Until it is loaded, find_encoder() returns nullptr and
+//    the caller runs the runtime-matrix GPU kernel instead, so no call ever
+//    waits for the compiler unless it asks to (ec_prepare_encoder).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <sys/stat.h>
+#include <thread>
+#include <tuple>
+#include <unistd.h>
+#include <vector>
+
+#include "rs_encoder.hpp"
+#include "rs_kernels.hpp"
+
+namespace uplink_ec {
+
+#define UPLINK_AOT(K, N) EncoderKernel aot_encoder_##K##_##N();
+#include "rs_encoder_aot.def"
+#undef UPLINK_AOT
+
+const EncoderKernel *aot_encoder(int k, int n) {
+    static const std::vector<EncoderKernel> table = {
+#define UPLINK_AOT(K, N) aot_encoder_##K##_##N(),
+#include "rs_encoder_aot.def"
+#undef UPLINK_AOT
+    };
+    for (const EncoderKernel &e : table)
+        if (e.k == k && e.n == n) return &e;
+    return nullptr;
+}
+
+bool encoder_supported(int k, int n) { return enc::supported(k, n); }
+
+namespace {
+
+#include "rs_jit_sources.inc"
+
+uint64_t fnv1a(uint64_t h, const void *p, size_t n) {
+    const unsigned char *b = (const unsigned char *)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+    return h;
+}
+
+std::string cache_dir() {
+    if (const char *d = getenv("UPLINK_EC_JIT_CACHE")) return d;
+    std::string base;
+    if (const char *x = getenv("XDG_CACHE_HOME")) base = x;
+    else if (const char *h = getenv("HOME")) base = std::string(h) + "/.cache";
+    else base = "/tmp";
+    return base + "/uplink_ec";
+}
+
+void mkdirs(const std::string &path) {
+    for (size_t i = 1; i <= path.size(); i++)
+        if (i == path.size() || path[i] == '/') (void)mkdir(path.substr(0, i).c_str(), 0755);
+}
+
+struct JitEntry {
+    enum State { kCompiling, kReady, kFailed } state = kCompiling;
+    std::vector<char> code;       // code object, both variants
+    std::string full_name, parity_name;
+    std::map<int, std::unique_ptr<EncoderKernel>> loaded;  // per device
+    std::map<int, hipModule_t> modules;
+};
+
+std::mutex g_mu;
+std::condition_variable g_cv;
+std::map<std::tuple<std::string, int, int>, std::unique_ptr<JitEntry>> g_jit;  // (arch, k, n)
+std::vector<std::thread> g_threads;  // compile threads (joined at exit)
+std::mutex g_compile_mu;             // one compilation at a time
+
+// Compile threads still running when the process exits must finish before the
+// HIP runtime tears itself down: the runtime registers its exit handler on its
+// first use, so this one, registered at the first compile (always later),
+// runs before it.
+void join_compiles() {
+    std::vector<std::thread> t;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        t.swap(g_threads);
+    }
+    for (auto &th : t)
+        if (th.joinable()) th.join();
+}
+
+std::string variant_expr(int k, int n, int nc) {
+    return "&uplink_ec::enc::rs_encode_special<" + std::to_string(k) + ", " + std::to_string(n) + ", " +
+           std::to_string(nc) + ", 4>";
+}
+
+// Compile (or read from the cache) the two variants of (k, n) for `arch`.
+void compile_entry(JitEntry *e, std::string arch, int k, int n) {
+    std::lock_guard<std::mutex> serial(g_compile_mu);
+    const std::string src = "#include \"rs_encoder.hpp\"\n";
+    const std::string full = variant_expr(k, n, 4), parity = variant_expr(k, n, enc::parity_compute_waves(k, n));
+    std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++20"};
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (int i = 0; i < kJitHeaderCount; i++) h = fnv1a(h, kJitHeaderTexts[i], strlen(kJitHeaderTexts[i]));
+    for (const auto &o : opts) h = fnv1a(h, o.data(), o.size());
+    h = fnv1a(h, full.data(), full.size());
+    h = fnv1a(h, parity.data(), parity.size());
+    int ver_major = 0, ver_minor = 0;
+    (void)hiprtcVersion(&ver_major, &ver_minor);
+    h = fnv1a(h, &ver_major, sizeof ver_major);
+    h = fnv1a(h, &ver_minor, sizeof ver_minor);
+    char hex[32];
+    snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
+    const std::string dir = cache_dir(), path = dir + "/enc_" + std::to_string(k) + "_" + std::to_string(n) + "_" + hex;
+    std::vector<char> code;
+    std::string names[2];
+    {
+        std::ifstream in(path + ".co", std::ios::binary);
+        std::ifstream nm(path + ".names");
+        if (in && nm && std::getline(nm, names[0]) && std::getline(nm, names[1]))
+            code.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+    }
+    if (code.empty()) {
+        hiprtcProgram prog;
+        bool ok = hiprtcCreateProgram(&prog, src.c_str(), "rs_encoder_jit.hip", kJitHeaderCount, kJitHeaderTexts,
+                                      kJitHeaderNames) == HIPRTC_SUCCESS;
+        if (ok) {
+            // one expression when both variants are the same instantiation (fewer than 32 parity rows)
+            ok = hiprtcAddNameExpression(prog, full.c_str()) == HIPRTC_SUCCESS &&
+                 (parity == full || hiprtcAddNameExpression(prog, parity.c_str()) == HIPRTC_SUCCESS);
+            std::vector<const char *> o;
+            for (const auto &s : opts) o.push_back(s.c_str());
+            if (ok && hiprtcCompileProgram(prog, (int)o.size(), o.data()) != HIPRTC_SUCCESS) {
+                size_t n_log = 0;
+                hiprtcGetProgramLogSize(prog, &n_log);
+                std::string log(n_log, '\0');
+                hiprtcGetProgramLog(prog, &log[0]);
+                fprintf(stderr, "uplink_ec: hiprtc failed for RS(%d,%d):\n%s\n", k, n, log.c_str());
+                ok = false;
+            }
+            const char *lowered[2] = {nullptr, nullptr};
+            if (ok) {
+                ok = hiprtcGetLoweredName(prog, full.c_str(), &lowered[0]) == HIPRTC_SUCCESS &&
+                     hiprtcGetLoweredName(prog, parity.c_str(), &lowered[1]) == HIPRTC_SUCCESS;
+                if (parity == full) lowered[1] = lowered[0];
+            }
+            size_t sz = 0;
+            if (ok) ok = hiprtcGetCodeSize(prog, &sz) == HIPRTC_SUCCESS && sz > 0;
+            if (ok) {
+                code.resize(sz);
+                ok = hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS;
+                names[0] = lowered[0];
+                names[1] = lowered[1];
+            }
+            hiprtcDestroyProgram(&prog);
+        }
+        if (!ok) code.clear();
+        if (!code.empty()) {  // publish atomically: write a temp file, rename
+            mkdirs(dir);
+            const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+            std::ofstream out(tmp + ".co", std::ios::binary);
+            out.write(code.data(), (std::streamsize)code.size());
+            std::ofstream nm(tmp + ".names");
+            nm << names[0] << "\n" << names[1] << "\n";
+            out.close();
+            nm.close();
+            if (out && nm) {
+                (void)rename((tmp + ".names").c_str(), (path + ".names").c_str());
+                (void)rename((tmp + ".co").c_str(), (path + ".co").c_str());
+            } else {
+                (void)remove((tmp + ".co").c_str());
+                (void)remove((tmp + ".names").c_str());
+            }
+        }
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    if (code.empty()) {
+        e->state = JitEntry::kFailed;
+    } else {
+        e->code = std::move(code);
+        e->full_name = names[0];
+        e->parity_name = names[1];
+        e->state = JitEntry::kReady;
+    }
+    g_cv.notify_all();
+}
+
+std::string device_arch(int dev) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return "";
+    std::string a = p.gcnArchName;
+    return a.substr(0, a.find(':'));
+}
+
+}  // namespace
+
+// Start (if needed) the run-time compilation of (k, n); with `wait`, block
+// until it is done.  Returns the encoder when it is loaded on the current
+// device, else nullptr.
+const EncoderKernel *jit_encoder(int k, int n, bool wait) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const std::string arch = device_arch(dev);
+    if (arch.empty()) return nullptr;
+    std::unique_lock<std::mutex> g(g_mu);
+    auto key = std::make_tuple(arch, k, n);
+    auto it = g_jit.find(key);
+    if (it == g_jit.end()) {
+        JitEntry *e = new JitEntry();
+        g_jit.emplace(key, std::unique_ptr<JitEntry>(e));
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(join_compiles); });
+        g_threads.emplace_back(compile_entry, e, arch, k, n);
+        it = g_jit.find(key);
+    }
+    JitEntry *e = it->second.get();
+    if (wait) g_cv.wait(g, [&] { return e->state != JitEntry::kCompiling; });
+    if (e->state != JitEntry::kReady) return nullptr;
+    auto ld = e->loaded.find(dev);
+    if (ld != e->loaded.end()) return ld->second.get();
+    hipModule_t mod = nullptr;
+    hipFunction_t f_full = nullptr, f_par = nullptr;
+    if (hipModuleLoadData(&mod, e->code.data()) != hipSuccess ||
+        hipModuleGetFunction(&f_full, mod, e->full_name.c_str()) != hipSuccess ||
+        hipModuleGetFunction(&f_par, mod, e->parity_name.c_str()) != hipSuccess) {
+        fprintf(stderr, "uplink_ec: loading the RS(%d,%d) encoder failed\n", k, n);
+        e->state = JitEntry::kFailed;
+        return nullptr;
+    }
+    e->modules[dev] = mod;
+    std::unique_ptr<EncoderKernel> ek(new EncoderKernel());
+    ek->k = k;
+    ek->n = n;
+    ek->jit = true;
+    const int pnc = enc::parity_compute_waves(k, n);
+    ek->full = {nullptr, f_full, 8 * 64, enc::wgs_per_cu(k), "rs_encode_special (jit)"};
+    ek->parity = {nullptr, f_par, (pnc + 4) * 64, enc::wgs_per_cu(k), "rs_encode_special (jit, parity only)"};
+    EncoderKernel *out = ek.get();
+    e->loaded[dev] = std::move(ek);
+    return out;
+}
+
+const EncoderKernel *find_encoder(int k, int n, bool wait) {
+    if (const EncoderKernel *e = aot_encoder(k, n)) return e;
+    if (!enc::supported(k, n)) return nullptr;
+    return jit_encoder(k, n, wait);
+}
+
+hipError_t launch_encode_special(const EncoderKernel &e, const RsArgs &args, int grid, hipStream_t s) {
+    const bool parity_only = args.copy_off[0] < 0;
+    const EncoderKernel::Variant &v = parity_only ? e.parity : e.full;
+    if (grid <= 0) grid = default_grid(args.total_tiles, v.wgs_per_cu);
+    RsArgs a = args;
+    void *params[] = {&a};
+    if (v.aot) return hipLaunchKernel(v.aot, dim3(grid), dim3(v.threads), params, 0, s);
+    return hipModuleLaunchKernel(v.jit, grid, 1, 1, v.threads, 1, 1, 0, s, params, nullptr);
+}
+
+}  // namespace uplink_ec

@@ -22,17 +22,24 @@
 //    256-byte share rows (coalesced).
 //
 // Two bodies share that skeleton:
-//  * rs_encode_special<K,N>: G is a compile-time constant (the same Lagrange
-//    construction as infectious, gf256.hpp), and each output plane gets the
-//    XOR of two precomputed 4-plane combinations ("four Russians"), one
-//    v_bitop3 per (output plane, input share): 8 ops per GF multiply-add of a
-//    32-byte column block instead of ~16 for the plain bit-matrix.
-//  * rs_matmul_jt<NW>: any runtime matrix (encode for arbitrary (k,n), and
-//    the rebuild matrix (G_S)^-1 of a share set).  Same four-Russians body,
-//    but the coefficient is data: each (row, input) pair is one call into a
-//    table of 256 compile-time leaves (rs_jump_table.inc), the accumulator
-//    row picked by VGPR index mode -- no per-bit branches.
+//  * rs_encode_special<K,N,..> (rs_encoder.hpp): G is a compile-time constant
+//    (the same Lagrange construction as infectious, gf256_field.hpp), and each
+//    output plane gets the XOR of two precomputed 4-plane combinations ("four
+//    Russians"), one v_bitop3 per (output plane, input share): 8 ops per GF
+//    multiply-add of a 32-byte column block instead of ~16 for the plain
+//    bit-matrix.  Library-built for the configurations of
+//    rs_encoder_aot.def, compiled by hiprtc for any other (k, n).
+//  * rs_matmul_jt<NW> (this file): any runtime matrix (the rebuild matrix
+//    (G_S)^-1 of a share set, re-encoding for error detection, per-stripe
+//    EncodeSingle).  Same four-Russians body, but the coefficient is data:
+//    each (row, input) pair is one call into a table of 256 compile-time
+//    leaves (rs_jump_table.inc), the accumulator row picked by VGPR index
+//    mode -- no per-bit branches.
+#include <hip/hip_runtime.h>
+
+#include "gf256_field.hpp"
 #include "rs_device.hpp"
+#include "rs_kernels.hpp"
 
 namespace uplink_ec {
 namespace {
@@ -40,63 +47,6 @@ namespace {
 using namespace dev;
 
 __constant__ GfTables d_gf = make_gf_tables();
-
-// Warp-specialised tile pipeline shared by both kernels: waves 0..3 compute
-// output rows, waves 4..7 ("loaders") fetch the next work item's input
-// chunks (non-temporal 16-B loads), write the systematic copies, bit-slice
-// them and fill the other slot of a 2-slot LDS ring.  One LDS-only barrier
-// per item, so loads of item i+1 and the stores of item i overlap the XOR
-// work of item i and nothing waits for store completion.
-// NC compute waves, NL loader waves.  4 + 4 for the full encode (memory-bound:
-// the loaders also write the k data pieces); 8 + 4 for the parity-only
-// encode, where the loaders have less to do and one compute wave per SIMD,
-// issuing at half rate on its own, would be the limit.
-template <int K, int N, int NC, int NL>
-__global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
-    constexpr int kNC = NC, kNL = NL;
-    constexpr int R = N - K;
-    constexpr int OPW = (R + kNC - 1) / kNC;
-    constexpr int PER = (K + kNL - 1) / kNL;
-    __shared__ uint32_t lds[2][K * 8 * 64];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool loader = wave >= kNC;
-    const int lw = wave - kNC;
-    int64_t tile = blockIdx.x;
-    if (loader && tile < a.total_tiles) {
-        const int64_t seg = tile / a.tiles_per_seg;
-        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
-        stage_inputs<kNL, PER, true>(a, seg, c, lds[0], lane, lw, 0, K, true);
-    }
-    lds_barrier();
-    int buf = 0;
-    for (; tile < a.total_tiles; tile += gridDim.x) {
-        if (loader) {
-            const int64_t next = tile + gridDim.x;
-            if (next < a.total_tiles) {
-                const int64_t seg = next / a.tiles_per_seg;
-                const TileCols c = tile_cols(a, next - seg * a.tiles_per_seg, lane);
-                stage_inputs<kNL, PER, true>(a, seg, c, lds[buf ^ 1], lane, lw, 0, K, true);
-            }
-        } else {
-            const int64_t seg = tile / a.tiles_per_seg;
-            const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
-            uint32_t acc[OPW][8];
-#pragma unroll
-            for (int o = 0; o < OPW; o++)
-#pragma unroll
-                for (int p = 0; p < 8; p++) acc[o][p] = 0;
-            static_for<kNC>([&]<int W>() {
-                if (wave == W) compute_special<K, N, OPW, W>(lds[buf], lane, acc);
-            });
-            const int rbase = wave * OPW;
-            const int cnt = R - rbase < OPW ? R - rbase : OPW;
-            store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
-        }
-        lds_barrier();
-        buf ^= 1;
-    }
-}
 
 // Runtime-matrix kernel (rebuild, and encode for (k, n) without a
 // specialised kernel).  Every wave computes (no loader waves) and several
@@ -136,10 +86,17 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             u32x8 acc[OPW];
 #pragma unroll
             for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
+            StageRegs<PER> r;
+            load_inputs<NW, PER, true>(a, seg, c, wave, 0, a.nin < JC ? a.nin : JC, r);
             for (int j0 = 0; j0 < a.nin; j0 += JC) {
                 const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
-                stage_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0);
+                slice_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
                 lds_barrier();
+                // the next chunk's loads are in flight while this chunk is multiplied in
+                if (j0 + JC < a.nin) {
+                    const int j1 = j0 + JC;
+                    load_inputs<NW, PER, true>(a, seg, c, wave, j1, a.nin - j1 < JC ? a.nin - j1 : JC, r);
+                }
                 if (cnt > 0)
                     jt_inputs(acc, lds_addr + (uint32_t)(buf * JC * 8 * 64 * 4),
                               a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
@@ -224,6 +181,8 @@ namespace uplink_ec {
 
 namespace {
 int g_cu_count = 0;
+}  // namespace
+
 int cu_count() {
     if (g_cu_count == 0) {
         int dev = 0, n = 0;
@@ -236,39 +195,10 @@ int cu_count() {
     return g_cu_count;
 }
 
-template <int K, int N>
-hipError_t launch_special(const RsArgs &a, int grid, hipStream_t s) {
-    // LDS ring = 2 * K * 2 KiB; one workgroup per CU for K = 29, two for small K
-    const int per_cu = (2 * K * 2048) * 2 <= 160 * 1024 ? 2 : 1;
-    if (grid <= 0) grid = default_grid(a.total_tiles, per_cu);
-    const bool parity_only = a.copy_off[0] < 0;
-#ifndef UPLINK_ENC_PO_NC
-#define UPLINK_ENC_PO_NC 8
-#endif
-    constexpr int PNC = UPLINK_ENC_PO_NC;
-    if (parity_only && N - K >= PNC * 4)
-        hipLaunchKernelGGL((rs_encode_special<K, N, PNC, 4>), dim3(grid), dim3((PNC + 4) * 64), 0, s, a);
-    else
-        hipLaunchKernelGGL((rs_encode_special<K, N, 4, 4>), dim3(grid), dim3(8 * 64), 0, s, a);
-    return hipGetLastError();
-}
-}  // namespace
-
 int default_grid(int64_t total_tiles, int wgs_per_cu) {
     int64_t g = (int64_t)cu_count() * wgs_per_cu;
     if (total_tiles < g) g = total_tiles;
     return (int)(g > 0 ? g : 1);
-}
-
-bool have_special_encoder(int k, int n) {
-    return (k == 29 && n == 80) || (k == 20 && n == 60) || (k == 4 && n == 10);
-}
-
-hipError_t launch_encode_special(int k, int n, const RsArgs &a, int grid, hipStream_t s) {
-    if (k == 29 && n == 80) return launch_special<29, 80>(a, grid, s);
-    if (k == 20 && n == 60) return launch_special<20, 60>(a, grid, s);
-    if (k == 4 && n == 10) return launch_special<4, 10>(a, grid, s);
-    return hipErrorInvalidValue;
 }
 
 size_t jt_targets_bytes(const RsArgs &a) {
@@ -282,18 +212,8 @@ hipError_t launch_jt_targets(const RsArgs &a, uint64_t *targets, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t s) {
-    RsArgs a = args;
-    uint64_t *own = nullptr;
-    if (!a.jt_tgt) {  // no prepared table: make one for this launch (stream-ordered)
-        hipError_t e = hipMallocAsync((void **)&own, jt_targets_bytes(a), s);
-        if (e != hipSuccess) return e;
-        if ((e = launch_jt_targets(a, own, s)) != hipSuccess) {
-            (void)hipFreeAsync(own, s);
-            return e;
-        }
-        a.jt_tgt = own;
-    }
+hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
+    if (!a.jt_tgt || a.nout > kMaxOps || a.nin > kMaxOps) return hipErrorInvalidValue;
     // up to 16 waves per CU (4 per SIMD: the jump-table body holds ~126
     // VGPRs); as few waves per workgroup as the rows need, since every wave
     // rebuilds the 4-plane combinations of each input for its own rows
@@ -310,9 +230,7 @@ hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t s) {
         if (grid <= 0) grid = default_grid(a.total_tiles, 4);
         hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
     }
-    hipError_t e = hipGetLastError();
-    if (own) (void)hipFreeAsync(own, s);  // runs after the kernel on s
-    return e;
+    return hipGetLastError();
 }
 
 hipError_t launch_matmul_bytes(const RsArgs &a, hipStream_t s) {

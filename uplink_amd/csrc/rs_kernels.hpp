@@ -1,70 +1,47 @@
-// Kernel argument block and launch entry points for the GF(2^8) Reed-Solomon
-// stripe kernels (encode K1, rebuild K2 in SURVEY.md §2).  Host-only header:
-// no torch types, plain pointers.
+// Launch entry points of the GF(2^8) Reed-Solomon stripe kernels (encode K1,
+// rebuild K2 in SURVEY.md §2).  Host-only header: no torch types, plain
+// pointers.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>
 
+#include "rs_args.hpp"
+
 namespace uplink_ec {
 
-// Max inputs / outputs of one launch (inputs = the k source shares, outputs =
-// the rows computed).  Larger row counts are split over several launches.
-constexpr int kMaxOps = 128;
-
-// One launch computes, for every byte column (stripe s, offset t < ess) of
-// every segment g in the batch:
-//   out_r[g, s, t] = XOR_j  M[r][j] * in_j[g, s, t]      (GF(2^8))
-// with
-//   in_j [g,s,t] = in_base  + g*in_seg_stride  + in_off[j]  + s*in_stripe_stride  + t
-//   out_r[g,s,t] = out_base + g*out_seg_stride + out_off[r] + s*out_stripe_stride + t
-// and, for inputs with copy_off[j] >= 0, the input bytes are also copied to
-//   out_base + g*out_seg_stride + copy_off[j] + s*out_stripe_stride + t
-// (the systematic pass-through of data shares: EncodeSingle num<k and
-// Rebuild's present data shares).
-//
-// Encode of a segment [stripe][k][ess] into pieces [n][stripes*ess]:
-//   in_off[j] = j*ess, in_stripe_stride = k*ess,
-//   out_off[r] = (k+r)*piece_len, copy_off[j] = j*piece_len,
-//   out_stripe_stride = ess.
-// Rebuild from pieces into a stripe-major segment swaps the two layouts.
-struct RsArgs {
-    const uint8_t *in_base;
-    uint8_t *out_base;
-    const uint8_t *coef;      // runtime matrix, coef[j*coef_ld + r] (generic kernel)
-    const uint64_t *jt_tgt;   // leaf addresses of coef (jt_targets_bytes; null: made per launch)
-    int64_t in_stripe_stride;
-    int64_t out_stripe_stride;
-    int64_t in_seg_stride;
-    int64_t out_seg_stride;
-    int64_t nstripes;         // stripes per segment
-    int64_t chunks_per_seg;   // nstripes * ess / 16
-    int64_t tiles_per_seg;    // ceil(chunks_per_seg / 128)
-    int64_t total_tiles;      // tiles_per_seg * nseg
-    int32_t ess;              // erasure share size, multiple of 16 for the bit-sliced path
-    int32_t cps;              // ess / 16 (16-byte chunks per share per stripe)
-    int32_t nin;              // number of inputs (k)
-    int32_t nout;             // number of computed rows
-    int32_t coef_ld;          // leading dimension of coef (multiple of 16)
-    int32_t pad_;
-    int64_t in_off[kMaxOps];  // bytes from in_base (16-byte aligned on the bit-sliced path)
-    int64_t out_off[kMaxOps]; // bytes from out_base
-    int64_t copy_off[kMaxOps];// bytes from out_base, -1 = no copy
+// A compile-time-G encoder of one (k, n) (rs_encoder.hpp): built into the
+// library for the configurations listed in rs_encoder_registry.cpp, compiled
+// with hiprtc for any other (k, n) on first use and cached on disk
+// (rs_encoder_jit.cpp).  Two variants: all n pieces, and parity only.
+struct EncoderKernel {
+    struct Variant {
+        const void *aot = nullptr;       // host stub of a library kernel
+        hipFunction_t jit = nullptr;     // function of a run-time module
+        int threads = 0;                 // workgroup size
+        int wgs_per_cu = 1;
+        const char *name = "";
+    };
+    int k = 0, n = 0;
+    bool jit = false;
+    Variant full, parity;
 };
 
-// Specialised compile-time-G encoders exist for these (k, n).
-bool have_special_encoder(int k, int n);
+// The encoder for (k, n) on the current device, or nullptr when (k, n) is
+// outside the compile-time encoder's limits or run-time compilation failed
+// (the caller then uses the runtime-matrix kernel).  Thread-safe.
+const EncoderKernel *find_encoder(int k, int n, bool wait = false);
+// Library-built encoders (rs_encoder_registry.cpp); nullptr if none.
+const EncoderKernel *aot_encoder(int k, int n);
+// The same limits find_encoder applies (no compilation).
+bool encoder_supported(int k, int n);
+hipError_t launch_encode_special(const EncoderKernel &e, const RsArgs &args, int grid, hipStream_t stream);
 
-// Launches.  `args.nout` rows of G (rows k..n-1) for the special encoder;
-// any matrix for the generic kernel.  Return hipError_t.
-hipError_t launch_encode_special(int k, int n, const RsArgs &args, int grid, hipStream_t stream);
+// Runtime-matrix kernel: args.coef / nin / nout with the leaf addresses of
+// that matrix in args.jt_tgt (made by launch_jt_targets into
+// jt_targets_bytes(args) bytes of device memory; required).
 hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t stream);
-// The generic kernel multiplies through a jump table whose leaf addresses
-// depend on the matrix: launch_jt_targets writes them for args.coef / nin /
-// nout into `targets` (jt_targets_bytes(args) bytes of device memory), after
-// which args.jt_tgt = targets lets any number of launches of that matrix skip
-// the per-launch preparation.
 size_t jt_targets_bytes(const RsArgs &args);
 hipError_t launch_jt_targets(const RsArgs &args, uint64_t *targets, hipStream_t stream);
 // Byte-wise fallback (any ess, any alignment); coef as above.
@@ -72,5 +49,6 @@ hipError_t launch_matmul_bytes(const RsArgs &args, hipStream_t stream);
 
 // Default grid (workgroups) for a launch over `total_tiles` tiles.
 int default_grid(int64_t total_tiles, int wgs_per_cu);
+int cu_count();
 
 }  // namespace uplink_ec

@@ -1,0 +1,192 @@
+// Device building blocks shared by the GF(2^8) stripe kernels: tile geometry,
+// the bit-slice transposes, LDS staging of input shares and the output of
+// computed rows.  Used by the compile-time-G encoders (rs_encoder.hpp, also
+// compiled at run time by hiprtc) and the runtime-matrix kernel
+// (rs_device.hpp / rs_kernels.hip); see rs_kernels.hip for the design notes.
+#pragma once
+#include "rs_args.hpp"
+
+namespace uplink_ec {
+namespace dev {
+
+// static_for<N>(f): f.template operator()<I>() for I = 0 .. N-1, unrolled at
+// compile time (clang's __make_integer_seq: no library header needed, so the
+// same code compiles under hiprtc).
+template <typename T, T... I>
+struct iseq {};
+template <typename F, int... I>
+__device__ __forceinline__ void sf_impl(F &&f, iseq<int, I...>) {
+    (f.template operator()<I>(), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    sf_impl(f, __make_integer_seq<iseq, int, N>{});
+}
+
+constexpr int kTileChunks = 128;  // 16-byte chunks per tile = 2048 byte columns
+
+__device__ __forceinline__ void swapmove(uint32_t &a, uint32_t &b, int s, uint32_t m) {
+    const uint32_t t = ((a >> s) ^ b) & m;
+    b ^= t;
+    a ^= t << s;
+}
+
+// 32 bytes (byte b of word w) -> 8 planes: plane p, bit 8b+w = bit p of byte (w,b).
+__device__ __forceinline__ void bitslice8(uint32_t (&w)[8]) {
+    swapmove(w[0], w[4], 4, 0x0F0F0F0Fu);
+    swapmove(w[1], w[5], 4, 0x0F0F0F0Fu);
+    swapmove(w[2], w[6], 4, 0x0F0F0F0Fu);
+    swapmove(w[3], w[7], 4, 0x0F0F0F0Fu);
+    swapmove(w[0], w[2], 2, 0x33333333u);
+    swapmove(w[1], w[3], 2, 0x33333333u);
+    swapmove(w[4], w[6], 2, 0x33333333u);
+    swapmove(w[5], w[7], 2, 0x33333333u);
+    swapmove(w[0], w[1], 1, 0x55555555u);
+    swapmove(w[2], w[3], 1, 0x55555555u);
+    swapmove(w[4], w[5], 1, 0x55555555u);
+    swapmove(w[6], w[7], 1, 0x55555555u);
+}
+
+// inverse of bitslice8 (each swap-move is an involution; reverse the stages)
+__device__ __forceinline__ void unbitslice8(uint32_t (&w)[8]) {
+    swapmove(w[0], w[1], 1, 0x55555555u);
+    swapmove(w[2], w[3], 1, 0x55555555u);
+    swapmove(w[4], w[5], 1, 0x55555555u);
+    swapmove(w[6], w[7], 1, 0x55555555u);
+    swapmove(w[0], w[2], 2, 0x33333333u);
+    swapmove(w[1], w[3], 2, 0x33333333u);
+    swapmove(w[4], w[6], 2, 0x33333333u);
+    swapmove(w[5], w[7], 2, 0x33333333u);
+    swapmove(w[0], w[4], 4, 0x0F0F0F0Fu);
+    swapmove(w[1], w[5], 4, 0x0F0F0F0Fu);
+    swapmove(w[2], w[6], 4, 0x0F0F0F0Fu);
+    swapmove(w[3], w[7], 4, 0x0F0F0F0Fu);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte global store; NT = non-temporal (streamed output written once,
+// never re-read by this kernel: keeps it from displacing useful lines).
+template <bool NT>
+__device__ __forceinline__ void st16(uint8_t *p, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    if constexpr (NT) {
+        __builtin_nontemporal_store((u32x4){x, y, z, w}, (u32x4 *)p);
+    } else {
+        *(uint4 *)p = make_uint4(x, y, z, w);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+    if constexpr (NT) {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *(const uint4 *)p;
+    }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations but, unlike __syncthreads() (whose release fence emits
+// s_waitcnt vmcnt(0)), does not drain outstanding global stores.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Checked build (UPLINK_EC_CHECKED, tests/test_c_abi.py): every 16-byte
+// global access of the stripe kernels is compared with the launch's declared
+// byte ranges; one outside them is skipped and its site recorded in
+// a.chk_flag, which the library reads after the launch.  In the product
+// build this is `true` and compiles away.
+__device__ __forceinline__ bool in_range(const RsArgs &a, const uint8_t *p, bool out, int site) {
+#ifdef UPLINK_EC_CHECKED
+    const uint8_t *lo = out ? a.chk_out_lo : a.chk_in_lo, *hi = out ? a.chk_out_hi : a.chk_in_hi;
+    if (p < lo || p + 16 > hi) {
+        if (a.chk_flag) atomicCAS(a.chk_flag, 0u, (uint32_t)site);
+        return false;
+    }
+#else
+    (void)a, (void)p, (void)out, (void)site;
+#endif
+    return true;
+}
+
+struct TileCols {
+    bool vA, vB;
+    int64_t inA, inB;    // byte offsets of the two chunks in an input share
+    int64_t outA, outB;  // byte offsets of the two chunks in an output row
+};
+
+__device__ __forceinline__ TileCols tile_cols(const RsArgs &a, int64_t tt, int lane) {
+    TileCols c;
+    const int64_t qA = tt * kTileChunks + lane;
+    const int64_t qB = qA + 64;
+    c.vA = qA < a.chunks_per_seg;
+    c.vB = qB < a.chunks_per_seg;
+    const uint32_t cps = (uint32_t)a.cps;
+    const uint32_t sA = (uint32_t)qA / cps, tA = (uint32_t)qA - sA * cps;
+    const uint32_t sB = (uint32_t)qB / cps, tB = (uint32_t)qB - sB * cps;
+    c.inA = (int64_t)sA * a.in_stripe_stride + (int64_t)tA * 16;
+    c.inB = (int64_t)sB * a.in_stripe_stride + (int64_t)tB * 16;
+    c.outA = (int64_t)sA * a.out_stripe_stride + (int64_t)tA * 16;
+    c.outB = (int64_t)sB * a.out_stripe_stride + (int64_t)tB * 16;
+    return c;
+}
+
+// Phase A: inputs j0 .. j0+jn-1 (thread handles j = j0 + wave + NW*i), load
+// two 16-byte chunks, optionally copy them through (systematic shares),
+// bit-slice and write the planes to lds[(j-j0)*8 + p][lane].
+template <int NW, int PER, bool NT = false>
+__device__ __forceinline__ void stage_inputs(const RsArgs &a, int64_t seg, const TileCols &c, uint32_t *lds,
+                                             int lane, int wave, int j0, int jn, bool do_copy) {
+    uint4 bufA[PER], bufB[PER];
+    const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int j = wave + NW * i;
+        if (j < jn) {
+            const uint8_t *p = in_seg + a.in_off[j0 + j];
+            bufA[i] = c.vA && in_range(a, p + c.inA, false, 1) ? ld16<NT>(p + c.inA) : z;
+            bufB[i] = c.vB && in_range(a, p + c.inB, false, 1) ? ld16<NT>(p + c.inB) : z;
+        }
+    }
+    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
+#pragma unroll
+    for (int i = 0; i < PER; i++) {
+        const int j = wave + NW * i;
+        if (j < jn) {
+            const int64_t co = a.copy_off[j0 + j];
+            if (do_copy && co >= 0) {
+                uint8_t *p = out_seg + co;
+                if (c.vA && in_range(a, p + c.outA, true, 2)) st16<NT>(p + c.outA, bufA[i].x, bufA[i].y, bufA[i].z, bufA[i].w);
+                if (c.vB && in_range(a, p + c.outB, true, 2)) st16<NT>(p + c.outB, bufB[i].x, bufB[i].y, bufB[i].z, bufB[i].w);
+            }
+            uint32_t w[8] = {bufA[i].x, bufA[i].y, bufA[i].z, bufA[i].w,
+                             bufB[i].x, bufB[i].y, bufB[i].z, bufB[i].w};
+            bitslice8(w);
+            uint32_t *dst = lds + j * 8 * 64 + lane;
+#pragma unroll
+            for (int p = 0; p < 8; p++) dst[p * 64] = w[p];
+        }
+    }
+}
+
+// Output: un-bit-slice each accumulated row and store its two chunks.
+template <int OPW, bool NT = false>
+__device__ __forceinline__ void store_rows(const RsArgs &a, int64_t seg, const TileCols &c, int rbase, int cnt,
+                                           uint32_t (&acc)[OPW][8]) {
+    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
+    static_for<OPW>([&]<int O>() {
+        if (O < cnt) {
+            uint32_t w[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) w[p] = acc[O][p];
+            unbitslice8(w);
+            uint8_t *p = out_seg + a.out_off[rbase + O];
+            if (c.vA && in_range(a, p + c.outA, true, 3)) st16<NT>(p + c.outA, w[0], w[1], w[2], w[3]);
+            if (c.vB && in_range(a, p + c.outB, true, 3)) st16<NT>(p + c.outB, w[4], w[5], w[6], w[7]);
+        }
+    });
+}
+
+}  // namespace dev
+}  // namespace uplink_ec
