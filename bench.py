@@ -93,9 +93,34 @@ def share_sets():
     return sets
 
 
+def cgroup_cpus():
+    """CPUs the cgroup quota grants this process (cgroup v2 cpu.max or v1
+    cfs quota), or None when unlimited / unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) / int(p)))
+            return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            p = int(fh.read())
+        return max(1, q // p) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def host_cpus():
-    """The cores this process may run on, and what they are (logged with the baseline)."""
-    cores = len(os.sched_getaffinity(0))
+    """The cores this process may run on -- its affinity set, capped by a
+    cgroup CPU quota when there is one -- and what they are (logged with the
+    baseline)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    cores = min(affinity, quota) if quota else affinity
     model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -105,7 +130,7 @@ def host_cpus():
                     break
     except OSError:
         pass
-    return cores, os.cpu_count() or cores, model
+    return cores, os.cpu_count() or cores, model, affinity, quota
 
 
 def cpu_baseline(min_s: float):
@@ -123,7 +148,7 @@ def cpu_baseline(min_s: float):
     nseg = 4
     segs = [np.frombuffer(rng.bytes(S_PAD), dtype=np.uint8) for _ in range(nseg)]
     sets = share_sets()
-    cores, nproc, model = host_cpus()
+    cores, nproc, model, affinity, quota = host_cpus()
 
     def run(threads, limit_s, fast=False, min_segs=1):
         t_enc = t_dec = 0.0
@@ -157,7 +182,8 @@ def cpu_baseline(min_s: float):
         "sample": f"{ref['segments']} x 64 MiB RS(29,80) segments ({nseg} distinct, cycled): oracle reference-shaped "
                   f"encode (EncodeSingle per piece per stripe, AVX2 PSHUFB addmul) + per-stripe Rebuild from the same "
                   f"29-piece sets as the GPU run; encode {ref['encode_s']}s, decode {ref['decode_s']}s wall on {cores} "
-                  f"threads (affinity set of this process; nproc {nproc}; {model})",
+                  f"threads (this process's CPUs: affinity {affinity}, cgroup quota {quota or 'none'}; nproc {nproc}; "
+                  f"{model})",
         "encode_gibps": ref["encode_gibps"],
         "decode_gibps": ref["decode_gibps"],
         "single_core": {"value": one["value"], "encode_gibps": one["encode_gibps"],
@@ -178,6 +204,60 @@ def oracle_spot_check(pieces_seg0: torch.Tensor, seg0: torch.Tensor, stripes: in
     ref = O.FEC(K, N).encode_segment(seg, ESS, threads=4)
     got = pieces_seg0[:, : stripes * ESS].cpu().numpy()
     return bool(np.array_equal(got, ref))
+
+
+def other_configs(L, dev, sptr, reps: int = 10):
+    """Informational, outside the timed region: the reference benchmark's
+    other configurations (private/eestream/rs_test.go:553-634: RS(20,50),
+    (30,60), (50,80)) on 8 x 64 MiB segments -- encode of all pieces and
+    rebuild from the last k pieces (all parity), HIP-event times per launch
+    and the HBM roofline fraction of each."""
+    out = {}
+    nseg = 8
+    for k, n in ((20, 50), (30, 60), (50, 80)):
+        stripe = k * ESS
+        nstripes = (RAW_SEGMENT + 4 + stripe - 1) // stripe
+        spad, plen = nstripes * stripe, nstripes * ESS
+        ctx = ctypes.c_void_p()
+        if L.ec_create(k, n, ESS, ctypes.byref(ctx)):
+            continue
+        segs = torch.randint(0, 256, (nseg, spad), dtype=torch.uint8, device=dev)
+        pcs = torch.empty((nseg, n, plen), dtype=torch.uint8, device=dev)
+        back = torch.empty((nseg, spad), dtype=torch.uint8, device=dev)
+        nums = (ctypes.c_int * k)(*range(n - k, n))
+        ptrs = (ctypes.c_void_p * k)(*[pcs.data_ptr() + j * plen for j in range(n - k, n)])
+
+        def enc():
+            assert L.ec_encode_segments(ctx, segs.data_ptr(), nseg, nstripes, pcs.data_ptr(), 0, sptr) == 0
+
+        def dec():
+            assert L.ec_rebuild_segments_batched(ctx, k, nums, ptrs, nstripes, nseg, n * plen, spad, back.data_ptr(),
+                                                 sptr) == 0
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        for _ in range(3):
+            enc()
+            dec()
+        ev[0].record()
+        for _ in range(reps):
+            enc()
+        ev[1].record()
+        for _ in range(reps):
+            dec()
+        ev[2].record()
+        ev[2].synchronize()
+        t_e = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+        t_d = ev[1].elapsed_time(ev[2]) / reps * 1e-3
+        eb, db = nseg * spad * (1 + n / k), nseg * spad * 2
+        out[f"RS({k},{n})"] = {
+            "encode_kernel": L.ec_encode_kernel_name(ctx).decode(),
+            "encode_us_per_segment": round(t_e / nseg * 1e6, 2), "encode_GBps": round(eb / t_e / 1e9, 1),
+            "encode_frac": round(eb / t_e / 1e9 / HBM_PEAK_GBPS, 4),
+            "rebuild_all_parity_us_per_segment": round(t_d / nseg * 1e6, 2), "rebuild_GBps": round(db / t_d / 1e9, 1),
+            "rebuild_frac": round(db / t_d / 1e9 / HBM_PEAK_GBPS, 4),
+            "verified": bool(torch.equal(back, segs))}
+        del segs, pcs, back
+        L.ec_destroy(ctx)
+    return out
 
 
 def main():
@@ -393,6 +473,8 @@ def main():
         "segments_timed_this_rank": seg_launched,
         "verified": verified,
     }
+    if rank == 0 and world == 1:
+        line["other_configs"] = other_configs(L, dev, sptr)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample_s)
     if rank == 0:

@@ -356,6 +356,34 @@ def test_concurrent_encode_single(oracle):
     assert not errors
 
 
+def test_coalesced_encode_single_mixed_sizes(oracle):
+    """ec_encode_single coalesces concurrent calls into batched launches
+    (group commit, grouped by share size): 48 threads with share sizes 256
+    (compile-time encoder), 64 and 100 (byte kernel), data and parity rows,
+    every result against the oracle."""
+    k, n = 29, 80
+    sch = scheme(k, n, 256)
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(13)
+    sizes = (256, 64, 100)
+    stripes = {bs: [rng.integers(0, 256, k * bs, dtype=np.uint8) for _ in range(4)] for bs in sizes}
+    errors = []
+
+    def work(t):
+        bs = sizes[t % len(sizes)]
+        out = np.zeros(bs, dtype=np.uint8)
+        for rep in range(25):
+            s = stripes[bs][(t + rep) % 4]
+            num = (t * 11 + rep * 17) % n
+            sch.encode_single(s, out, num)
+            if not np.array_equal(out, f.encode_single(s, num)):
+                errors.append((t, rep, bs, num))
+    th = [threading.Thread(target=work, args=(t,)) for t in range(48)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+
+
 def _pinned(lib, nbytes):
     p = lib.ec_host_alloc(nbytes)
     assert p

@@ -69,3 +69,30 @@ def test_two_rank_gloo_sharded_encode(oracle):
     for g, v in merged.items():
         seg = np.random.default_rng(segment_seed(g)).integers(0, 256, 3 * 4 * 64, dtype=np.uint8)
         assert v == f.encode_segment(seg, 64).tobytes()
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
+    """The bench's N > 1 path with the HIP engine: two ranks (torch
+    distributed run) share the box's one GPU and use gloo for the barrier and
+    the max over ranks; each rank encodes and rebuilds its own contiguous
+    shard of 64 segments (32 each) with no data-path collective, and the
+    rank-0 line reports the whole job.  The driver's multi-GPU runs use RCCL
+    (the default backend) on one GPU per rank."""
+    import json
+    import subprocess
+    import sys
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
+           "2", "--warmup", "1", "--settle-s", "0", "--total-segments", "64", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["verified"] is True
+    assert line["config"]["total_segments_per_step"] == 64 and line["config"]["segments_this_rank"] == 32
+    assert line["value"] > 0

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <list>
@@ -49,7 +50,19 @@ using PlanPtr = std::shared_ptr<MatPlan>;
 struct Workspace {
     uint8_t *d_buf = nullptr;
     size_t cap = 0;
+    uint8_t *h_buf = nullptr;  // pinned staging for the per-stripe calls' host buffers
+    size_t h_cap = 0;
     hipStream_t stream = nullptr;
+};
+
+// EncodeSingle requests waiting for a batched launch (ec_encode_single).
+struct SingleReq {
+    const uint8_t *in;
+    size_t bs;
+    uint8_t *out;
+    int num;
+    int rc = EC_OK;
+    bool done = false;
 };
 
 // Every export that takes a context runs on the context's device and
@@ -90,6 +103,12 @@ struct ec_ctx {
     std::vector<Workspace *> free_ws;
     std::vector<std::unique_ptr<Workspace>> all_ws;
     uint32_t *d_chk = nullptr;     // checked build: the kernels' violation word
+    // EncodeSingle coalescing (group commit): callers queue, one of them runs
+    // everything queued as one batch while the next batch queues up
+    std::mutex single_mu;
+    std::condition_variable single_cv;
+    std::vector<SingleReq *> single_q;
+    bool single_busy = false;
 };
 
 namespace {
@@ -112,7 +131,7 @@ int hip_fail(hipError_t e) {
         if (e_ != hipSuccess) return hip_fail(e_);   \
     } while (0)
 
-Workspace *acquire_ws(ec_ctx *c, size_t need) {
+Workspace *acquire_ws(ec_ctx *c, size_t need, size_t host_need = 0) {
     Workspace *w = nullptr;
     {
         std::lock_guard<std::mutex> g(c->mu);
@@ -131,6 +150,13 @@ Workspace *acquire_ws(ec_ctx *c, size_t need) {
         w->cap = 0;
         size_t cap = std::max(need, (size_t)1 << 20);
         if (hipMalloc(&w->d_buf, cap) == hipSuccess) w->cap = cap;
+    }
+    if (host_need && w->h_cap < host_need) {
+        if (w->h_buf) (void)hipHostFree(w->h_buf);
+        w->h_buf = nullptr;
+        w->h_cap = 0;
+        size_t cap = std::max(host_need, (size_t)1 << 20);
+        if (hipHostMalloc((void **)&w->h_buf, cap, hipHostMallocDefault) == hipSuccess) w->h_cap = cap;
     }
     return w;
 }
@@ -455,6 +481,7 @@ void ec_destroy(ec_ctx *c) {
     for (auto &w : c->all_ws) {
         if (w->stream) (void)hipStreamSynchronize(w->stream), (void)hipStreamDestroy(w->stream);
         if (w->d_buf) (void)hipFree(w->d_buf);
+        if (w->h_buf) (void)hipHostFree(w->h_buf);
     }
     c->plans.clear();
     c->enc_parity.reset();
@@ -626,7 +653,91 @@ static int pipe_drain(ec_ctx *c, int rc) {
     return rc;
 }
 
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
 // ---------------------------------------------------------------- per-stripe
+// One launch sequence for EncodeSingle requests of one share size bs: the
+// stripes are packed into pinned staging, copied in with one transfer, the
+// parity of every stripe is encoded in one launch (the compile-time encoder
+// where there is one), a gather kernel picks each request's share, and one
+// transfer brings them back.
+static int run_single_batch(ec_ctx *c, SingleReq *const *req, size_t nreq, size_t bs) {
+    const int k = c->k, n = c->n;
+    const size_t stripe = (size_t)k * bs;
+    const size_t in_bytes = nreq * stripe, par_bytes = (size_t)(n - k) * nreq * bs, out_bytes = nreq * bs;
+    // device: [stripes | nums | parity | out]; pinned host: [stripes | nums | out]
+    const size_t nums_at = align_up(in_bytes, 256), par_at = nums_at + align_up(nreq * 4, 256);
+    const size_t out_at = par_at + align_up(par_bytes, 256), h_out = par_at;
+    Workspace *w = acquire_ws(c, out_at + out_bytes + 64, h_out + out_bytes);
+    if (!w->d_buf || !w->stream || !w->h_buf) {
+        release_ws(c, w);
+        return EC_ERR_DEVICE;
+    }
+    for (size_t r = 0; r < nreq; r++) {
+        memcpy(w->h_buf + r * stripe, req[r]->in, stripe);
+        ((int *)(w->h_buf + nums_at))[r] = req[r]->num;
+    }
+    uint8_t *d = w->d_buf;
+    hipStream_t st = w->stream;
+    int rc = EC_OK;
+    do {
+        if (hipMemcpyAsync(d, w->h_buf, nums_at + nreq * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+            rc = EC_ERR_DEVICE;
+            break;
+        }
+        if (n > k) {  // parity of every stripe of the batch
+            RsArgs a{};
+            a.in_base = d;
+            a.out_base = d + par_at;
+            a.in_stripe_stride = (int64_t)stripe;
+            a.out_stripe_stride = (int64_t)bs;
+            a.nin = k;
+            a.nout = n - k;
+            for (int j = 0; j < k; j++) a.in_off[j] = (int64_t)j * bs, a.copy_off[j] = -1;
+            std::vector<int64_t> out_off(n - k);
+            for (int r = 0; r < n - k; r++) out_off[r] = (int64_t)r * nreq * bs;
+            for (int r = 0; r < std::min(n - k, kMaxOps); r++) a.out_off[r] = out_off[r];
+            fill_geometry(a, (int)bs, (int64_t)nreq, 1);
+            const bool bits = bs % 16 == 0;
+            const EncoderKernel *ek = bits ? find_encoder(k, n) : nullptr;
+            if (ek) {
+                set_extents(a, 1, c->d_chk);
+                if (launch_encode_special(*ek, a, 0, st) != hipSuccess) {
+                    rc = EC_ERR_DEVICE;
+                    break;
+                }
+                rc = after_launch(c->d_chk, st);
+            } else {
+                if (!bits) a.cps = 1;
+                PlanPtr plan;
+                rc = parity_plan(c, &plan);
+                if (rc == EC_OK) rc = run_matmul(c, a, out_off.data(), *plan, 1, bits, st);
+            }
+            if (rc) break;
+        }
+        if (launch_gather_shares(d, d + par_at, (const int *)(d + nums_at), k, (int64_t)nreq, (int64_t)bs, d + out_at,
+                                 st) != hipSuccess ||
+            hipMemcpyAsync(w->h_buf + h_out, d + out_at, out_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            rc = EC_ERR_DEVICE;
+            break;
+        }
+        for (size_t r = 0; r < nreq; r++) memcpy(req[r]->out, w->h_buf + h_out + r * bs, bs);
+    } while (0);
+    if (rc) (void)hipStreamSynchronize(st);
+    release_ws(c, w);
+    return rc;
+}
+
+constexpr size_t kMaxSingleBatch = 2048;
+
+// EncodeSingle (rs.go:21-23), called by uplink per (piece, stripe) from up to
+// 300 goroutines at once (segmentupload/encode.go:58, testuplink/uplink.go:83).
+// Concurrent calls are coalesced by group commit: a caller that finds no batch
+// running takes every queued request (its own included) and runs them as one
+// batch; calls arriving meanwhile queue for the next one.  A lone caller pays
+// one transfer-kernel-transfer round trip; many callers share it
+// (tools/bench_per_stripe.py).
 int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len, int num) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!c) return EC_ERR_INVALID_ARG;
@@ -639,31 +750,34 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
     if (!in || !out) return EC_ERR_INVALID_ARG;
     if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
     DeviceGuard dg(c->device);
-    PlanPtr plan;
-    int rc = row_plan(c, num, &plan);
-    if (rc) return rc;
-    Workspace *w = acquire_ws(c, in_len + bs + 64);
-    if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
-    const size_t out_at = (in_len + 15) & ~(size_t)15;
-    do {
-        if (hipMemcpyAsync(w->d_buf, in, in_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-        RsArgs a{};
-        a.in_base = w->d_buf;
-        a.out_base = w->d_buf + out_at;
-        a.in_stripe_stride = (int64_t)in_len;
-        a.out_stripe_stride = (int64_t)bs;
-        for (int j = 0; j < c->k; j++) { a.in_off[j] = (int64_t)j * bs; a.copy_off[j] = -1; }
-        const int64_t out_off = 0;
-        fill_geometry(a, (int)bs, 1, 1);
-        const bool bits = (bs % 16) == 0;
-        if (!bits) a.cps = 1;
-        rc = run_matmul(c, a, &out_off, *plan, 1, bits, w->stream);
-        if (rc) break;
-        if (hipMemcpyAsync(out, w->d_buf + out_at, bs, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
-    } while (0);
-    release_ws(c, w);
-    return rc;
+    SingleReq r{in, bs, out, num};
+    std::unique_lock<std::mutex> lk(c->single_mu);
+    c->single_q.push_back(&r);
+    while (!r.done) {
+        if (c->single_busy) {
+            c->single_cv.wait(lk);
+            continue;
+        }
+        c->single_busy = true;
+        const size_t take = std::min(c->single_q.size(), kMaxSingleBatch);
+        std::vector<SingleReq *> batch(c->single_q.begin(), c->single_q.begin() + take);
+        c->single_q.erase(c->single_q.begin(), c->single_q.begin() + take);
+        lk.unlock();
+        // group by share size (one launch sequence per size)
+        std::stable_sort(batch.begin(), batch.end(), [](const SingleReq *a, const SingleReq *b) { return a->bs < b->bs; });
+        for (size_t i = 0; i < batch.size();) {
+            size_t j = i;
+            while (j < batch.size() && batch[j]->bs == batch[i]->bs) j++;
+            const int rc = run_single_batch(c, batch.data() + i, j - i, batch[i]->bs);
+            for (size_t q = i; q < j; q++) batch[q]->rc = rc;
+            i = j;
+        }
+        lk.lock();
+        for (SingleReq *q : batch) q->done = true;
+        c->single_busy = false;
+        c->single_cv.notify_all();
+    }
+    return r.rc;
 }
 
 int ec_encode(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out) {
@@ -729,21 +843,24 @@ int ec_rebuild(const ec_ctx *cc, int nshares, int *nums, const uint8_t **shares,
     if (!out) return EC_ERR_INVALID_ARG;
     const size_t slot = (share_len + 15) & ~(size_t)15;
     const size_t out_at = slot * nshares;
-    Workspace *w = acquire_ws(c, out_at + share_len * c->k + 64);
-    if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
+    // the shares go through pinned staging in one transfer each way
+    Workspace *w = acquire_ws(c, out_at + share_len * c->k + 64, out_at + share_len * c->k);
+    if (!w->d_buf || !w->stream || !w->h_buf) { release_ws(c, w); return EC_ERR_DEVICE; }
     int rc = EC_OK;
     do {
         std::vector<const uint8_t *> dptr(nshares);
         for (int i = 0; i < nshares; i++) {
-            if (hipMemcpyAsync(w->d_buf + slot * i, shares[i], share_len, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            memcpy(w->h_buf + slot * i, shares[i], share_len);
             dptr[i] = w->d_buf + slot * i;
         }
-        if (rc) break;
+        if (hipMemcpyAsync(w->d_buf, w->h_buf, out_at, hipMemcpyHostToDevice, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, w->d_buf + out_at, w->stream);
         if (rc) break;
-        if (hipMemcpyAsync(out, w->d_buf + out_at, share_len * c->k, hipMemcpyDeviceToHost, w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-        if (hipStreamSynchronize(w->stream) != hipSuccess) rc = EC_ERR_DEVICE;
+        if (hipMemcpyAsync(w->h_buf + out_at, w->d_buf + out_at, share_len * c->k, hipMemcpyDeviceToHost, w->stream) != hipSuccess ||
+            hipStreamSynchronize(w->stream) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        memcpy(out, w->h_buf + out_at, share_len * c->k);
     } while (0);
+    if (rc) (void)hipStreamSynchronize(w->stream);
     release_ws(c, w);
     return rc;
 }
@@ -766,7 +883,6 @@ void ec_host_free(void *p) {
 // kernel, then D2H, all stream-ordered, so a slot's device buffers are never
 // reused before its previous segment has left the GPU; the three streams
 // overlap the copies of neighbouring segments with each other and the kernel.
-static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // BLAKE3 of every piece of one segment resident on the device: parity pieces
 // are contiguous in `parity` ([n-k][plen]), data piece j is share j of every

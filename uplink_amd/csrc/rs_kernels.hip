@@ -173,6 +173,22 @@ __global__ __launch_bounds__(256) void rs_matmul_bytes(const RsArgs a) {
     }
 }
 
+// Batched EncodeSingle (ec_encode_single's coalesced calls): share nums[r]
+// of stripe r, from the stripe itself (a data share) or from the parity
+// pieces of the batch ([n-k][B*bs]), into out[r]; 16-byte units when bs allows.
+__global__ __launch_bounds__(256) void rs_gather_shares(const uint8_t *stripes, const uint8_t *parity, const int *nums,
+                                                        int k, int64_t nreq, int64_t bs, uint8_t *out) {
+    const bool wide = (bs & 15) == 0;
+    const int64_t unit = wide ? 16 : 1, per = bs / unit, total = nreq * per;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / per, t = (i - r * per) * unit;
+        const int num = nums[r];
+        const uint8_t *src = num < k ? stripes + (r * k + num) * bs + t : parity + ((int64_t)(num - k) * nreq + r) * bs + t;
+        if (wide) *(uint4 *)(out + r * bs + t) = *(const uint4 *)src;
+        else out[r * bs + t] = *src;
+    }
+}
+
 }  // namespace
 }  // namespace uplink_ec
 
@@ -230,6 +246,16 @@ hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
         if (grid <= 0) grid = default_grid(a.total_tiles, 4);
         hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_shares(const uint8_t *stripes, const uint8_t *parity, const int *nums, int k, int64_t nreq,
+                               int64_t bs, uint8_t *out, hipStream_t s) {
+    const int64_t units = nreq * ((bs & 15) == 0 ? bs / 16 : bs);
+    int64_t blocks = (units + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(rs_gather_shares, dim3((unsigned)blocks), dim3(256), 0, s, stripes, parity, nums, k, nreq, bs, out);
     return hipGetLastError();
 }
 

@@ -46,6 +46,10 @@ size_t jt_targets_bytes(const RsArgs &args);
 hipError_t launch_jt_targets(const RsArgs &args, uint64_t *targets, hipStream_t stream);
 // Byte-wise fallback (any ess, any alignment); coef as above.
 hipError_t launch_matmul_bytes(const RsArgs &args, hipStream_t stream);
+// out[r] (bs bytes) = share nums[r] of stripe r: stripes [nreq][k][bs],
+// parity pieces [n-k][nreq*bs] (batched EncodeSingle)
+hipError_t launch_gather_shares(const uint8_t *stripes, const uint8_t *parity, const int *nums, int k, int64_t nreq,
+                               int64_t bs, uint8_t *out, hipStream_t stream);
 
 // Default grid (workgroups) for a launch over `total_tiles` tiles.
 int default_grid(int64_t total_tiles, int wgs_per_cu);
