@@ -10,7 +10,7 @@
 // v_bitop3 per output plane that XORs a precomputed 4-plane combination of the
 // low nibble with one of the high nibble ("four Russians").
 //
-// Warp-specialised: NC compute waves own the parity rows (OPW each); NL
+// Warp-specialised: NC compute waves own the parity rows (rows_of); NL
 // loader waves fetch the next work item's inputs (non-temporal 16-B loads),
 // write the systematic data pieces straight from registers, bit-slice and
 // fill the other slot of a 2-slot LDS ring.  A work item is a chunk of up to
@@ -30,13 +30,24 @@ namespace enc {
 
 using namespace dev;
 
-constexpr int kMaxChunk = 36;  // input shares per LDS slot: 2 slots x 36 x 2 KiB = 144 KiB
+// UPLINK_ENC_* overrides are for developer experiments (tools/exp/enc_variants.py)
+#ifndef UPLINK_ENC_MAX_CHUNK
+#define UPLINK_ENC_MAX_CHUNK 36
+#endif
+constexpr int kMaxChunk = UPLINK_ENC_MAX_CHUNK;  // input shares per LDS slot: 2 slots x 36 x 2 KiB = 144 KiB
 constexpr int chunks_of(int K) { return (K + kMaxChunk - 1) / kMaxChunk; }
 constexpr int chunk_size(int K) { return (K + chunks_of(K) - 1) / chunks_of(K); }
 
-// acc[O] ^= G[K + W*OPW + O][J] * x_J for the inputs J0 .. J0+JN-1, whose bit
-// planes sit in lds at slot J - J0.
-template <int K, int N, int OPW, int W, int J0, int JN>
+// Parity rows of compute wave W of NC: R = N - K rows dealt as evenly as
+// possible (the first R % NC waves take one more), so the two compute waves
+// that share a SIMD in the 8-wave form carry 12-13 rows each for RS(29,80)
+// instead of 14 and 9.
+constexpr int rows_of(int R, int NC, int W) { return R / NC + (W < R % NC ? 1 : 0); }
+constexpr int rbase_of(int R, int NC, int W) { return W * (R / NC) + (W < R % NC ? W : R % NC); }
+
+// acc[O] ^= G[K + rbase + O][J] * x_J for the wave's rows and the inputs
+// J0 .. J0+JN-1, whose bit planes sit in lds at slot J - J0.
+template <int K, int N, int NC, int OPW, int W, int J0, int JN>
 __device__ __forceinline__ void compute_chunk(const uint32_t *lds, int lane, uint32_t (&acc)[OPW][8]) {
     static_for<JN>([&]<int JJ>() {
         constexpr int J = J0 + JJ;
@@ -58,8 +69,8 @@ __device__ __forceinline__ void compute_chunk(const uint32_t *lds, int lane, uin
             }
         });
         static_for<OPW>([&]<int O>() {
-            constexpr int r = W * OPW + O;
-            if constexpr (r < N - K) {
+            constexpr int r = rbase_of(N - K, NC, W) + O;
+            if constexpr (O < rows_of(N - K, NC, W)) {
                 constexpr uint8_t cval = gen_entry(K, K + r, J);
                 static_for<8>([&]<int P>() {
                     constexpr uint8_t row = mul_bitrow(cval, P);
@@ -120,15 +131,14 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
                 if (ch == C) {
                     constexpr int J0 = C * KC, JN = K - J0 < KC ? K - J0 : KC;
                     static_for<NC>([&]<int W>() {
-                        if (wave == W) compute_chunk<K, N, OPW, W, J0, JN>(lds[buf], lane, acc);
+                        if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN>(lds[buf], lane, acc);
                     });
                 }
             });
             if (ch == NCH - 1) {
                 const int64_t seg = tile / a.tiles_per_seg;
                 const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
-                const int rbase = wave * OPW;
-                const int cnt = R - rbase < OPW ? R - rbase : OPW;
+                const int rbase = rbase_of(R, NC, wave), cnt = rows_of(R, NC, wave);
                 store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
             }
         }
@@ -148,7 +158,13 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // (DESIGN.md §4).
 constexpr int parity_compute_waves(int k, int n) { return n - k >= 32 ? 8 : 4; }
 // Workgroups per CU the LDS ring allows (one workgroup per CU above 80 KiB).
-constexpr int wgs_per_cu(int k) { return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 ? 2 : 1; }
+constexpr int wgs_per_cu(int k) {
+#ifdef UPLINK_ENC_WGS_PER_CU
+    return UPLINK_ENC_WGS_PER_CU;
+#else
+    return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 ? 2 : 1;
+#endif
+}
 
 }  // namespace enc
 }  // namespace uplink_ec

@@ -133,7 +133,9 @@ __device__ __forceinline__ TileCols tile_cols(const RsArgs &a, int64_t tt, int l
 
 // Phase A: inputs j0 .. j0+jn-1 (thread handles j = j0 + wave + NW*i), load
 // two 16-byte chunks, optionally copy them through (systematic shares),
-// bit-slice and write the planes to lds[(j-j0)*8 + p][lane].
+// bit-slice and write the planes to lds[(j-j0)*8 + p][lane].  All loads are
+// issued before the first is consumed (issuing them in smaller groups
+// measured slower: tools/exp/enc_variants.py).
 template <int NW, int PER, bool NT = false>
 __device__ __forceinline__ void stage_inputs(const RsArgs &a, int64_t seg, const TileCols &c, uint32_t *lds,
                                              int lane, int wave, int j0, int jn, bool do_copy) {
