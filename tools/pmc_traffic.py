@@ -45,12 +45,14 @@ def family(match):
 
 res = {
     "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of `python3 bench.py "
-              f"--steps 3 --warmup 1 --settle-s 0 --no-cpu-baseline` ({B} RS(29,80) 64 MiB segments per launch); mean "
+              f"--steps 3 --warmup 1 --settle-s 0 --no-cpu-baseline --no-other-configs` ({B} RS(29,80) 64 MiB segments per launch); mean "
               "over dispatches; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py",
     "segments_per_launch": B,
     "encode": family("rs_encode_special<29, 80, 4, 4>"),
     "decode": family("rs_matmul_jt"),
-    "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD},
+    "encode_parity_only": family("rs_encode_special<29, 80, 8, 4>"),
+    "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD,
+                    "encode_parity_only": int(B * S_PAD * (1 + (N - K) / K))},
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: (v["hbm_bytes_per_launch"] if isinstance(v, dict) and "hbm_bytes_per_launch" in v else v)

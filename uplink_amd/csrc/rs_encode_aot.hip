@@ -11,13 +11,6 @@
 #define UPLINK_AOT_NAME2(K, N) aot_encoder_##K##_##N
 #define UPLINK_AOT_NAME(K, N) UPLINK_AOT_NAME2(K, N)
 
-#ifndef UPLINK_ENC_FULL_NC
-#define UPLINK_ENC_FULL_NC 4
-#endif
-#ifndef UPLINK_ENC_FULL_NL
-#define UPLINK_ENC_FULL_NL 4
-#endif
-
 namespace uplink_ec {
 
 EncoderKernel UPLINK_AOT_NAME(UPLINK_AOT_K, UPLINK_AOT_N)() {
@@ -27,11 +20,8 @@ EncoderKernel UPLINK_AOT_NAME(UPLINK_AOT_K, UPLINK_AOT_N)() {
     EncoderKernel e;
     e.k = K;
     e.n = N;
-    constexpr int FNC = UPLINK_ENC_FULL_NC, FNL = UPLINK_ENC_FULL_NL;
-    e.full = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, FNC, FNL>), nullptr, (FNC + FNL) * 64,
-              enc::wgs_per_cu(K),
-              "rs_encode_special<" UPLINK_STR(UPLINK_AOT_K) "," UPLINK_STR(UPLINK_AOT_N) "," UPLINK_STR(
-                  UPLINK_ENC_FULL_NC) "," UPLINK_STR(UPLINK_ENC_FULL_NL) ">"};
+    e.full = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, 4, 4>), nullptr, 8 * 64,
+              enc::wgs_per_cu(K), "rs_encode_special<" UPLINK_STR(UPLINK_AOT_K) "," UPLINK_STR(UPLINK_AOT_N) ",4,4>"};
     e.parity = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, PNC, 4>), nullptr, (PNC + 4) * 64,
                 enc::wgs_per_cu(K),
                 PNC == 8 ? "rs_encode_special<" UPLINK_STR(UPLINK_AOT_K) "," UPLINK_STR(UPLINK_AOT_N) ",8,4>"

@@ -30,11 +30,7 @@ namespace enc {
 
 using namespace dev;
 
-// UPLINK_ENC_* overrides are for developer experiments (tools/exp/enc_variants.py)
-#ifndef UPLINK_ENC_MAX_CHUNK
-#define UPLINK_ENC_MAX_CHUNK 36
-#endif
-constexpr int kMaxChunk = UPLINK_ENC_MAX_CHUNK;  // input shares per LDS slot: 2 slots x 36 x 2 KiB = 144 KiB
+constexpr int kMaxChunk = 36;  // input shares per LDS slot: 2 slots x 36 x 2 KiB = 144 KiB
 constexpr int chunks_of(int K) { return (K + kMaxChunk - 1) / kMaxChunk; }
 constexpr int chunk_size(int K) { return (K + chunks_of(K) - 1) / chunks_of(K); }
 
@@ -158,13 +154,7 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // (DESIGN.md §4).
 constexpr int parity_compute_waves(int k, int n) { return n - k >= 32 ? 8 : 4; }
 // Workgroups per CU the LDS ring allows (one workgroup per CU above 80 KiB).
-constexpr int wgs_per_cu(int k) {
-#ifdef UPLINK_ENC_WGS_PER_CU
-    return UPLINK_ENC_WGS_PER_CU;
-#else
-    return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 ? 2 : 1;
-#endif
-}
+constexpr int wgs_per_cu(int k) { return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 ? 2 : 1; }
 
 }  // namespace enc
 }  // namespace uplink_ec
