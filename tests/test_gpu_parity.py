@@ -542,13 +542,14 @@ def test_reference_bench_configs_use_library_encoders(oracle, k, n):
     assert np.array_equal(gpu_encode(sch, seg, parity_only=True).cpu().numpy()[0], ref[k:])
 
 
-@pytest.mark.parametrize("k,n,stripes", [(5, 9, 33), (37, 50, 17), (10, 20, 1025)])
+@pytest.mark.parametrize("k,n,stripes", [(5, 9, 33), (37, 50, 17), (10, 20, 1025), (3, 70, 40)])
 def test_run_time_compiled_encoder(oracle, k, n, stripes):
     """(k, n) without a library-built encoder: compiled by hiprtc from the
     same header text (waited for here), then bit-exact vs the oracle, for all
     pieces and parity only, batched over 3 segments.  RS(37,50) needs two
-    input chunks.  Before it is ready the same calls run the runtime-matrix
-    kernel (test_encode_rebuild_vs_oracle covers that path)."""
+    input chunks; RS(3,70) has more parity rows than 4 compute waves hold
+    (the 8 + 4 full encoder).  Before it is ready the same calls run the
+    runtime-matrix kernel (test_encode_rebuild_vs_oracle covers that path)."""
     ess = 256
     sch = scheme(k, n, ess)
     assert sch._lib.ec_prepare_encoder(sch._ctx, 1) == 1
@@ -571,5 +572,9 @@ def test_prepare_encoder_reports_limits():
     sch = scheme(7, 200, 256)
     assert sch._lib.ec_prepare_encoder(sch._ctx, 0) == 0
     assert _kernel_name(sch) == "generic"
+    # k > 48: the two-chunk compiled body is no faster than the runtime-matrix kernel there
+    s3 = scheme(60, 80, 256)
+    assert s3._lib.ec_prepare_encoder(s3._ctx, 0) == 0
+    assert _kernel_name(s3) == "generic"
     s2 = scheme(29, 80, 256)
     assert s2._lib.ec_prepare_encoder(s2._ctx, 0) == 1

@@ -33,7 +33,7 @@ def main(src, out):
             continue
         med = {n: statistics.median(x) for n, x in c.items()}
         e = {"dispatches": max(len(x) for x in c.values()), "counters": med}
-        if "SQ_WAVE_CYCLES" in med:
+        if "SQ_WAVE_CYCLES" in med and "SQ_WAIT_ANY" in med:
             e["wait_share"] = round(med["SQ_WAIT_ANY"] / med["SQ_WAVE_CYCLES"], 3)
             e["valu_active_share"] = round(med["SQ_ACTIVE_INST_VALU"] / med["SQ_WAVE_CYCLES"], 3)
             e["issue_stall_share"] = round(med["SQ_WAIT_INST_ANY"] / med["SQ_WAVE_CYCLES"], 3)

@@ -16,11 +16,12 @@ namespace uplink_ec {
 EncoderKernel UPLINK_AOT_NAME(UPLINK_AOT_K, UPLINK_AOT_N)() {
     constexpr int K = UPLINK_AOT_K, N = UPLINK_AOT_N;
     static_assert(enc::supported(K, N), "outside the compile-time encoder's limits");
-    constexpr int PNC = enc::parity_compute_waves(K, N);
+    constexpr int PNC = enc::parity_compute_waves(K, N), FNC = enc::full_compute_waves(K, N);
+    static_assert(FNC == 4, "library-built configurations use the 4 + 4 full encoder (its kernel name below)");
     EncoderKernel e;
     e.k = K;
     e.n = N;
-    e.full = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, 4, 4>), nullptr, 8 * 64,
+    e.full = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, FNC, 4>), nullptr, (FNC + 4) * 64,
               enc::wgs_per_cu(K), "rs_encode_special<" UPLINK_STR(UPLINK_AOT_K) "," UPLINK_STR(UPLINK_AOT_N) ",4,4>"};
     e.parity = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, PNC, 4>), nullptr, (PNC + 4) * 64,
                 enc::wgs_per_cu(K),

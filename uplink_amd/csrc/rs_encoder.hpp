@@ -153,6 +153,12 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // on its own, is the limit: 8 + 4 waves once there are >= 32 parity rows
 // (DESIGN.md §4).
 constexpr int parity_compute_waves(int k, int n) { return n - k >= 32 ? 8 : 4; }
+// Compute waves of the full encode: 4, one per SIMD beside a loader wave,
+// while a wave's rows fit its registers next to the loaders' (<= 13 rows:
+// RS(29,80) runs at 198 VGPRs, two waves per SIMD); more parity rows would
+// spill (RS(10,100) at 23 rows per wave: 120 B per lane to scratch), so
+// 8 compute waves then.
+constexpr int full_compute_waves(int k, int n) { return n - k > 52 ? 8 : 4; }
 // Workgroups per CU the LDS ring allows (one workgroup per CU above 80 KiB).
 constexpr int wgs_per_cu(int k) { return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 ? 2 : 1; }
 

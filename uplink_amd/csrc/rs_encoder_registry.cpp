@@ -112,7 +112,8 @@ std::string variant_expr(int k, int n, int nc) {
 void compile_entry(JitEntry *e, std::string arch, int k, int n) {
     std::lock_guard<std::mutex> serial(g_compile_mu);
     const std::string src = "#include \"rs_encoder.hpp\"\n";
-    const std::string full = variant_expr(k, n, 4), parity = variant_expr(k, n, enc::parity_compute_waves(k, n));
+    const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n)),
+                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n));
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++20"};
     uint64_t h = 0xcbf29ce484222325ull;
     for (int i = 0; i < kJitHeaderCount; i++) h = fnv1a(h, kJitHeaderTexts[i], strlen(kJitHeaderTexts[i]));
@@ -246,17 +247,23 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
     ek->k = k;
     ek->n = n;
     ek->jit = true;
-    const int pnc = enc::parity_compute_waves(k, n);
-    ek->full = {nullptr, f_full, 8 * 64, enc::wgs_per_cu(k), "rs_encode_special (jit)"};
+    const int pnc = enc::parity_compute_waves(k, n), fnc = enc::full_compute_waves(k, n);
+    ek->full = {nullptr, f_full, (fnc + 4) * 64, enc::wgs_per_cu(k), "rs_encode_special (jit)"};
     ek->parity = {nullptr, f_par, (pnc + 4) * 64, enc::wgs_per_cu(k), "rs_encode_special (jit, parity only)"};
     EncoderKernel *out = ek.get();
     e->loaded[dev] = std::move(ek);
     return out;
 }
 
+// Run-time compilation is worth it up to k = 48 inputs: measured against the
+// runtime-matrix kernel (tools/bench_jit.py) the compiled
+// encoder is 10-25 % faster there, while at k = 56-64 the two-chunk body is no
+// faster and takes a minute of hiprtc time.
+constexpr int kJitMaxK = 48;
+
 const EncoderKernel *find_encoder(int k, int n, bool wait) {
     if (const EncoderKernel *e = aot_encoder(k, n)) return e;
-    if (!enc::supported(k, n)) return nullptr;
+    if (!enc::supported(k, n) || k > kJitMaxK) return nullptr;
     return jit_encoder(k, n, wait);
 }
 
