@@ -14,6 +14,7 @@
 #include <cstring>
 #include <list>
 #include <memory>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -55,6 +56,12 @@ struct Workspace {
     hipStream_t stream = nullptr;
 };
 
+// A caller waiting for a workspace (acquire_ws).
+struct WsWaiter {
+    std::condition_variable cv;
+    Workspace *w = nullptr;
+};
+
 // EncodeSingle requests waiting for a batched launch (ec_encode_single).
 struct SingleReq {
     const uint8_t *in;
@@ -62,7 +69,9 @@ struct SingleReq {
     uint8_t *out;
     int num;
     int rc = EC_OK;
+    bool taken = false;  // in a batch a leader is running
     bool done = false;
+    std::condition_variable cv;  // this caller's wake-up (done, or its turn to lead)
 };
 
 // Every export that takes a context runs on the context's device and
@@ -102,13 +111,13 @@ struct ec_ctx {
     std::vector<PlanPtr> enc_row;  // row num of G (EncodeSingle)
     std::vector<Workspace *> free_ws;
     std::vector<std::unique_ptr<Workspace>> all_ws;
+    std::deque<WsWaiter *> ws_waiters;  // callers waiting for a workspace, first come first served
     uint32_t *d_chk = nullptr;     // checked build: the kernels' violation word
-    // EncodeSingle coalescing (group commit): callers queue, one of them runs
-    // everything queued as one batch while the next batch queues up
+    // EncodeSingle coalescing (group commit): callers queue; up to
+    // kSingleLeaders of them at a time each run everything queued as one batch
     std::mutex single_mu;
-    std::condition_variable single_cv;
-    std::vector<SingleReq *> single_q;
-    bool single_busy = false;
+    std::deque<SingleReq *> single_q;
+    int single_leaders = 0;
 };
 
 namespace {
@@ -131,16 +140,28 @@ int hip_fail(hipError_t e) {
         if (e_ != hipSuccess) return hip_fail(e_);   \
     } while (0)
 
+// At most kMaxWorkspaces per context: each has its own stream, and beyond a
+// few the streams only share the device's hardware queues (GPU_MAX_HW_QUEUES,
+// 4) while every new one costs a stream and pinned memory.  Callers beyond
+// that wait in arrival order and get a workspace handed over on release, so no
+// caller starves (300 threads of per-stripe calls: DESIGN.md §5a).
+constexpr size_t kMaxWorkspaces = 8;
+
 Workspace *acquire_ws(ec_ctx *c, size_t need, size_t host_need = 0) {
     Workspace *w = nullptr;
     {
-        std::lock_guard<std::mutex> g(c->mu);
+        std::unique_lock<std::mutex> g(c->mu);
         if (!c->free_ws.empty()) {
             w = c->free_ws.back();
             c->free_ws.pop_back();
-        } else {
+        } else if (c->all_ws.size() < kMaxWorkspaces) {
             c->all_ws.emplace_back(new Workspace());
             w = c->all_ws.back().get();
+        } else {
+            WsWaiter me;
+            c->ws_waiters.push_back(&me);
+            me.cv.wait(g, [&] { return me.w != nullptr; });
+            w = me.w;
         }
     }
     if (!w->stream && hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) w->stream = nullptr;
@@ -163,6 +184,13 @@ Workspace *acquire_ws(ec_ctx *c, size_t need, size_t host_need = 0) {
 
 void release_ws(ec_ctx *c, Workspace *w) {
     std::lock_guard<std::mutex> g(c->mu);
+    if (!c->ws_waiters.empty()) {
+        WsWaiter *next = c->ws_waiters.front();
+        c->ws_waiters.pop_front();
+        next->w = w;
+        next->cv.notify_one();
+        return;
+    }
     c->free_ws.push_back(w);
 }
 
@@ -730,14 +758,18 @@ static int run_single_batch(ec_ctx *c, SingleReq *const *req, size_t nreq, size_
 }
 
 constexpr size_t kMaxSingleBatch = 2048;
+constexpr int kSingleLeaders = 2;  // batches in flight at once: one's host copies overlap the other's GPU work
 
 // EncodeSingle (rs.go:21-23), called by uplink per (piece, stripe) from up to
 // 300 goroutines at once (segmentupload/encode.go:58, testuplink/uplink.go:83).
-// Concurrent calls are coalesced by group commit: a caller that finds no batch
-// running takes every queued request (its own included) and runs them as one
-// batch; calls arriving meanwhile queue for the next one.  A lone caller pays
-// one transfer-kernel-transfer round trip; many callers share it
-// (tools/bench_per_stripe.py).
+// Concurrent calls are coalesced by group commit: a caller that finds fewer
+// than kSingleLeaders batches running becomes a leader, takes every queued
+// request (its own included) and runs them as one batch; calls arriving
+// meanwhile queue for the next one.  Each caller sleeps on its own condition
+// variable and is woken once -- when its result is ready, or when it heads the
+// queue and a leader slot frees -- so 300 waiting threads cost no thundering
+// herd.  A lone caller pays one transfer-kernel-transfer round trip; many
+// callers share it (tools/per_stripe_bench.c).
 int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len, int num) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!c) return EC_ERR_INVALID_ARG;
@@ -754,14 +786,15 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
     std::unique_lock<std::mutex> lk(c->single_mu);
     c->single_q.push_back(&r);
     while (!r.done) {
-        if (c->single_busy) {
-            c->single_cv.wait(lk);
+        if (r.taken || c->single_leaders >= kSingleLeaders) {
+            r.cv.wait(lk);
             continue;
         }
-        c->single_busy = true;
+        c->single_leaders++;
         const size_t take = std::min(c->single_q.size(), kMaxSingleBatch);
         std::vector<SingleReq *> batch(c->single_q.begin(), c->single_q.begin() + take);
         c->single_q.erase(c->single_q.begin(), c->single_q.begin() + take);
+        for (SingleReq *q : batch) q->taken = true;
         lk.unlock();
         // group by share size (one launch sequence per size)
         std::stable_sort(batch.begin(), batch.end(), [](const SingleReq *a, const SingleReq *b) { return a->bs < b->bs; });
@@ -773,9 +806,13 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
             i = j;
         }
         lk.lock();
-        for (SingleReq *q : batch) q->done = true;
-        c->single_busy = false;
-        c->single_cv.notify_all();
+        c->single_leaders--;
+        for (SingleReq *q : batch) {
+            q->done = true;
+            if (q != &r) q->cv.notify_one();
+        }
+        // the leader slot passes to the oldest queued caller
+        if (!c->single_q.empty()) c->single_q.front()->cv.notify_one();
     }
     return r.rc;
 }
