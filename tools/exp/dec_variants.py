@@ -1,7 +1,7 @@
 """Developer experiment: time the RS(29,80) rebuild (16 x 64 MiB segments per
 launch, bench.py's layout) for share sets with m = 0 .. 29 missing data
-shares in library variants (tools/exp/build_enc_variants.sh with
--DUPLINK_REBUILD_WS=0/1 ...), interleaved so box drift cancels; every
+shares in library variants (tools/exp/build_enc_variants.sh), interleaved
+so box drift cancels; every
 rebuild is checked against the segments it came from.
   python tools/exp/dec_variants.py tools/exp/bin/var_*/libuplink_ec.so
 """

@@ -1,6 +1,5 @@
 """Developer experiment: time the RS(29,80) encode (full and parity-only,
-16 x 64 MiB segments per launch, as bench.py) in library variants built with
-UPLINK_ENC_* knobs (rs_encoder.hpp, rs_encode_aot.hip) by
+16 x 64 MiB segments per launch, as bench.py) in library variants built by
 tools/exp/build_enc_variants.sh, interleaved A/B/A/B so box drift cancels, and
 check every variant's pieces against the product library's.
   python tools/exp/enc_variants.py tools/exp/bin/var_*/libuplink_ec.so
