@@ -1,7 +1,8 @@
-"""Developer experiment: time the RS(29,80) encode (full and parity-only,
-16 x 64 MiB segments per launch, as bench.py) in library variants built by
-tools/exp/build_enc_variants.sh, interleaved A/B/A/B so box drift cancels, and
-check every variant's pieces against the product library's.
+"""Developer experiment: time the compile-time encoder (full and parity-only,
+16 x 64 MiB segments per launch, as bench.py) for RS(29,80) and the reference
+benchmark's library-built configurations in library variants built by
+tools/exp/build_enc_variants.sh, interleaved A/B/A/B so box drift cancels,
+and check every variant's pieces against the product library's.
   python tools/exp/enc_variants.py tools/exp/bin/var_*/libuplink_ec.so
 """
 import ctypes
@@ -12,8 +13,11 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-import bench as B  # noqa: E402
 from uplink_amd import _native  # noqa: E402
+
+CONFIGS = [(29, 80), (20, 50), (30, 60), (50, 80)]
+ESS = 256
+RAW = 64 << 20
 
 
 def load(path):
@@ -28,52 +32,62 @@ def load(path):
 def main(paths):
     dev = torch.device("cuda", 0)
     nb = 16
-    segs = B.padded_segments(nb, 0, dev)
-    pieces = torch.empty((nb, B.N, B.PIECE), dtype=torch.uint8, device=dev)
-    ref = None
     s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    bufs = {}
+    for k, n in CONFIGS:
+        stripes = (RAW + 4 + k * ESS - 1) // (k * ESS)
+        segs = torch.randint(0, 256, (nb, stripes * k * ESS), dtype=torch.uint8, device=dev, generator=g)
+        bufs[(k, n)] = (stripes, segs, torch.empty((nb, n, stripes * ESS), dtype=torch.uint8, device=dev))
     libs = []
+    refs = {}
     for p in [_native.LIB_PATH] + paths:
         L = load(p)
-        ctx = ctypes.c_void_p()
-        assert L.ec_create(B.K, B.N, B.ESS, ctypes.byref(ctx)) == 0
-        pieces.zero_()
-        assert L.ec_encode_segments(ctx, segs.data_ptr(), nb, B.NSTRIPES, pieces.data_ptr(), 0, s) == 0
-        torch.cuda.synchronize()
-        if ref is None:
-            ref = pieces.clone()
-            ok = True
-        else:
-            ok = bool(torch.equal(pieces, ref))
         tag = os.path.basename(os.path.dirname(p)) if p != _native.LIB_PATH else "product"
-        print(f"{tag:28s} kernel={L.ec_encode_kernel_name(ctx).decode()!r} pieces_equal={ok}", flush=True)
-        libs.append((tag, L, ctx))
+        ctxs = {}
+        for (k, n), (stripes, segs, pieces) in bufs.items():
+            ctx = ctypes.c_void_p()
+            assert L.ec_create(k, n, ESS, ctypes.byref(ctx)) == 0
+            ctxs[(k, n)] = ctx
+            pieces.zero_()
+            assert L.ec_encode_segments(ctx, segs.data_ptr(), nb, stripes, pieces.data_ptr(), 0, s) == 0
+            torch.cuda.synchronize()
+            if (k, n) not in refs:
+                refs[(k, n)] = pieces.clone()
+            else:
+                assert torch.equal(pieces, refs[(k, n)]), (tag, k, n)
+        print(f"{tag:20s} pieces equal to the product's for {CONFIGS}", flush=True)
+        libs.append((tag, L, ctxs))
 
-    def t(L, ctx, flags, it=20):
+    def t(L, ctx, kn, flags, it=20):
+        stripes, segs, pieces = bufs[kn]
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         for _ in range(3):
-            L.ec_encode_segments(ctx, segs.data_ptr(), nb, B.NSTRIPES, pieces.data_ptr(), flags, s)
+            L.ec_encode_segments(ctx, segs.data_ptr(), nb, stripes, pieces.data_ptr(), flags, s)
         e0.record()
         for _ in range(it):
-            L.ec_encode_segments(ctx, segs.data_ptr(), nb, B.NSTRIPES, pieces.data_ptr(), flags, s)
+            L.ec_encode_segments(ctx, segs.data_ptr(), nb, stripes, pieces.data_ptr(), flags, s)
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / it / nb
 
-    res = {tag: {"full": [], "parity": []} for tag, _, _ in libs}
+    res = {(tag, kn, f): [] for tag, _, _ in libs for kn in CONFIGS for f in (0, 1)}
     for rnd in range(3):
-        for tag, L, ctx in libs:
-            res[tag]["full"].append(t(L, ctx, 0))
-            res[tag]["parity"].append(t(L, ctx, _native.EC_FLAG_PARITY_ONLY))
-    full_bytes = B.S_PAD * (1 + B.N / B.K)
-    par_bytes = B.S_PAD * (1 + (B.N - B.K) / B.K)
-    for tag, r in res.items():
-        f = min(r["full"])
-        pa = min(r["parity"])
-        print(f"{tag:28s} full {f:6.2f} us/seg ({full_bytes / f / 1e6:5.3f} TB/s)  "
-              f"parity {pa:6.2f} us/seg ({par_bytes / pa / 1e6:5.3f} TB/s)   all: "
-              f"{' '.join(f'{x:.1f}' for x in r['full'])} | {' '.join(f'{x:.1f}' for x in r['parity'])}", flush=True)
+        for tag, L, ctxs in libs:
+            for kn in CONFIGS:
+                res[(tag, kn, 0)].append(t(L, ctxs[kn], kn, 0))
+                res[(tag, kn, 1)].append(t(L, ctxs[kn], kn, _native.EC_FLAG_PARITY_ONLY))
+    print("us per segment (min of 3 rounds), TB/s algorithmic; full | parity-only")
+    for kn in CONFIGS:
+        k, n = kn
+        stripes = bufs[kn][0]
+        sp = stripes * k * ESS
+        for tag, _, _ in libs:
+            f, pa = min(res[(tag, kn, 0)]), min(res[(tag, kn, 1)])
+            print(f"RS{kn!s:9s} {tag:20s} full {f:6.2f} ({sp * (1 + n / k) / f / 1e6:5.3f})  "
+                  f"parity {pa:6.2f} ({sp * (1 + (n - k) / k) / pa / 1e6:5.3f})", flush=True)
 
 
 if __name__ == "__main__":
