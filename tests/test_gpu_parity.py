@@ -384,6 +384,43 @@ def test_coalesced_encode_single_mixed_sizes(oracle):
     assert not errors, errors[:5]
 
 
+def test_concurrent_rebuild_and_decode_more_threads_than_workspaces(oracle):
+    """40 threads of per-stripe Rebuild and Decode on one context -- more
+    callers than its 8 workspaces, so most of them wait and are handed a
+    workspace in arrival order -- with random share sets and, for Decode, one
+    corrupted share; every result against the stripe it came from."""
+    k, n, ess = 29, 80, 256
+    sch = scheme(k, n, ess)
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(17)
+    stripes = [rng.integers(0, 256, k * ess, dtype=np.uint8) for _ in range(6)]
+    allsh = [f.encode(s) for s in stripes]
+    errors = []
+
+    def work(t):
+        r = np.random.default_rng(1000 + t)
+        for rep in range(10):
+            i = (t + rep) % len(stripes)
+            if t % 2 == 0:
+                nums = sorted(r.choice(n, k, replace=False).tolist())
+                got = np.zeros(k * ess, dtype=np.uint8)
+
+                def put(sh, got=got):
+                    got[sh.number * ess:(sh.number + 1) * ess] = sh.data
+                sch.rebuild([eestream.Share(j, np.array(allsh[i][j])) for j in nums], put)
+            else:
+                nums = sorted(r.choice(n, k + 4, replace=False).tolist())
+                sh = [eestream.Share(j, np.array(allsh[i][j])) for j in nums]
+                sh[int(r.integers(0, len(sh)))].data[int(r.integers(0, ess))] ^= 0x5A
+                got = sch.decode(None, sh)
+            if not np.array_equal(np.asarray(got).reshape(-1), stripes[i]):
+                errors.append((t, rep))
+    th = [threading.Thread(target=work, args=(t,)) for t in range(40)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+
+
 def _pinned(lib, nbytes):
     p = lib.ec_host_alloc(nbytes)
     assert p
@@ -542,13 +579,15 @@ def test_reference_bench_configs_use_library_encoders(oracle, k, n):
     assert np.array_equal(gpu_encode(sch, seg, parity_only=True).cpu().numpy()[0], ref[k:])
 
 
-@pytest.mark.parametrize("k,n,stripes", [(5, 9, 33), (37, 50, 17), (10, 20, 1025), (3, 70, 40)])
+@pytest.mark.parametrize("k,n,stripes", [(5, 9, 33), (37, 50, 17), (10, 20, 1025), (3, 70, 40), (36, 40, 9),
+                                          (2, 98, 7)])
 def test_run_time_compiled_encoder(oracle, k, n, stripes):
     """(k, n) without a library-built encoder: compiled by hiprtc from the
     same header text (waited for here), then bit-exact vs the oracle, for all
     pieces and parity only, batched over 3 segments.  RS(37,50) needs two
-    input chunks; RS(3,70) has more parity rows than 4 compute waves hold
-    (the 8 + 4 full encoder).  Before it is ready the same calls run the
+    input chunks; RS(36,40) is the largest single chunk; RS(3,70) and
+    RS(2,98) (96 parity rows, the limit) have more parity rows than 4 compute
+    waves hold (the 8 + 4 full encoder).  Before it is ready the same calls run the
     runtime-matrix kernel (test_encode_rebuild_vs_oracle covers that path)."""
     ess = 256
     sch = scheme(k, n, ess)
