@@ -451,6 +451,20 @@ def main():
         "avg_us_back_to_back": round(t_par_b2b * 1e6, 2),
         "bytes_per_launch": int(par_bytes), "achieved_GBps": round(par_bytes / t_par / 1e9, 1),
         "frac": par_frac, "note": "informational, not in value"}
+    # an on-box copy kernel next to the spec peak (torch's device copy of 1 GiB,
+    # read + write bytes; outside the timed region)
+    cpy_a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    cpy_b = torch.empty_like(cpy_a)
+    for _ in range(3):
+        cpy_b.copy_(cpy_a)
+    ce = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ce[0].record(stream)
+    for _ in range(10):
+        cpy_b.copy_(cpy_a)
+    ce[1].record(stream)
+    ce[1].synchronize()
+    copy_gbps = 2 * (1 << 30) * 10 / (ce[0].elapsed_time(ce[1]) * 1e-3) / 1e9
+    del cpy_a, cpy_b
     dominant = "encode" if t_enc_full >= t_dec_full else "decode"
     dk = kernels[dominant]
     traffic = None
@@ -483,7 +497,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(dk["achieved_GBps"], 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "frac_parity_only_encode": par_frac,
-                     "frac_decode": round(dec_gbps / HBM_PEAK_GBPS, 4)},
+                     "frac_decode": round(dec_gbps / HBM_PEAK_GBPS, 4),
+                     "copy_GBps_on_box": round(copy_gbps, 1),
+                     "frac_of_copy": round(dk["achieved_GBps"] / copy_gbps, 4)},
         "kernels": kernels,
         "encode_gibps": round(B * S_PAD / 2**30 / t_enc_full, 2),
         "decode_gibps": round(B * S_PAD / 2**30 / t_dec_full, 2),
