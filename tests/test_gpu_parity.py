@@ -75,6 +75,8 @@ CONFIGS = [  # (k, n, ess, stripes): reference test configs + BASEL
     (7, 200, 256, 2),    # 193 parity rows: split over launches
     (29, 80, 256, 1),    # a single stripe (tile tail)
     (29, 80, 256, 129),  # ragged tile count
+    (64, 96, 256, 17),   # k > 48: runtime-matrix encoder (no run-time compilation)
+    (128, 256, 256, 3),  # the limits: 128 inputs, 128 parity rows (4 passes of 32), all-parity rebuild of 128 rows
 ]
 
 
