@@ -65,6 +65,48 @@ __global__ __launch_bounds__(256) void rd(const v4 *in, v4 *out, int64_t n) {
     if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) out[0] = acc;
 }
 
+// write-only: W stores of consecutive 1 KiB wave blocks per thread
+template <int W, bool NT>
+__global__ __launch_bounds__(256) void wr(v4 *out, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+        const int64_t i = (wave * W + w) * 64 + lane;
+        if (i < n) st<NT>(out + i, v4{(uint32_t)i, (uint32_t)w, 1u, 2u});
+    }
+}
+
+// the same with the blocks interleaved over all waves: store w of every wave
+// lands in one dense front (block w * total_waves + wave)
+template <int W>
+__global__ __launch_bounds__(256) void wr_il(v4 *out, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+        const int64_t i = (w * tw + wave) * 64 + lane;
+        if (i < n) st<true>(out + i, v4{(uint32_t)i, (uint32_t)w, 1u, 2u});
+    }
+}
+template <int R, int W>
+__global__ __launch_bounds__(256) void mix_il(const v4 *in, v4 *out, int64_t n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    v4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const int64_t i = (r * tw + wave) * 64 + lane;
+        if (i < n) acc ^= ld<true>(in + i);
+    }
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+        const int64_t i = (w * tw + wave) * 64 + lane;
+        if (i < n / R * W) st<true>(out + i, acc ^ (uint32_t)w);
+    }
+}
 
 // persistent form: one workgroup of WPC waves per CU, each wave loops over
 // blocks of R read / W written 1 KiB wave-chunks (the data-piece stores of
@@ -194,8 +236,33 @@ int main() {
     MIX(1, 1, 0) MIX(1, 1, 1) MIX(4, 4, 0) MIX(4, 4, 1)
     MIX(29, 80, 1) MIX(29, 80, 0) MIX(4, 11, 1) MIX(1, 3, 1) MIX(1, 3, 0)
     MIX(29, 51, 1) MIX(4, 7, 1)
-    // write-only: R=1 read of a tiny stride (n small) is not expressible here;
-    // W/R = 3 with R=1 is the write-dominated end.
+#define WR(W, NT)                                                                                              \
+    {                                                                                                          \
+        const int64_t wn = WB / 16, waves = wn / 64 / (W);                                                     \
+        char nm[96];                                                                                           \
+        snprintf(nm, sizeof nm, "write-only W=%d nt=%d (3 GiB)", W, NT);                                       \
+        timeit(nm, (double)WB, [&] { hipLaunchKernelGGL((wr<W, NT>), dim3((waves + 3) / 4), dim3(256), 0, 0, B, wn); }); \
+    }
+    WR(1, 0) WR(1, 1) WR(4, 1) WR(16, 1)
+#define WRIL(W)                                                                                                \
+    {                                                                                                          \
+        const int64_t wn = WB / 16, waves = wn / 64 / (W);                                                     \
+        char nm[96];                                                                                           \
+        snprintf(nm, sizeof nm, "write-only interleaved W=%d (3 GiB)", W);                                     \
+        timeit(nm, (double)WB, [&] { hipLaunchKernelGGL((wr_il<W>), dim3((waves + 3) / 4), dim3(256), 0, 0, B, wn); }); \
+    }
+    WRIL(4) WRIL(16)
+#define MIXIL(R, W)                                                                                            \
+    {                                                                                                          \
+        const int64_t waves = n / 64 / (R);                                                                    \
+        char nm[96];                                                                                           \
+        snprintf(nm, sizeof nm, "mix interleaved R=%d W=%d (w:r %.2f)", R, W, (double)(W) / (R));              \
+        timeit(nm, (double)RB * (1.0 + (double)(W) / (R)), [&] {                                               \
+            hipLaunchKernelGGL((mix_il<R, W>), dim3((waves + 3) / 4), dim3(256), 0, 0, A, B, n);               \
+        });                                                                                                    \
+    }
+    MIXIL(4, 11) MIXIL(29, 80) MIXIL(29, 51) MIXIL(4, 4)
+    timeit("hipMemsetAsync 3 GiB", (double)WB, [&] { CK(hipMemsetAsync(B, 0x11, WB, 0)); });
 
 #define LOOP(R, W, WPC)                                                                                        \
     {                                                                                                          \
