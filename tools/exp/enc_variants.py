@@ -8,6 +8,7 @@ and check every variant's pieces against the product library's.
 import ctypes
 import os
 import sys
+import time
 
 import torch
 
@@ -15,7 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from uplink_amd import _native  # noqa: E402
 
-CONFIGS = [(29, 80), (20, 50), (30, 60), (50, 80)]
+CONFIGS = [(29, 80), (20, 50), (30, 60), (50, 80), (20, 60)]
+if os.environ.get("ENC_ONLY"):  # e.g. ENC_ONLY=50,80
+    CONFIGS = [tuple(int(x) for x in os.environ["ENC_ONLY"].split(","))]
+COOL_S = float(os.environ.get("ENC_COOL_S", "0"))  # idle time before each timed loop
 ESS = 256
 RAW = 64 << 20
 
@@ -62,6 +66,8 @@ def main(paths):
 
     def t(L, ctx, kn, flags, it=20):
         stripes, segs, pieces = bufs[kn]
+        if COOL_S:
+            time.sleep(COOL_S)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         for _ in range(3):
@@ -77,8 +83,10 @@ def main(paths):
     for rnd in range(3):
         for tag, L, ctxs in libs:
             for kn in CONFIGS:
-                res[(tag, kn, 0)].append(t(L, ctxs[kn], kn, 0))
-                res[(tag, kn, 1)].append(t(L, ctxs[kn], kn, _native.EC_FLAG_PARITY_ONLY))
+                # ENC_PO_FIRST=1 times the parity-only launch before the full one (the launch
+                # timed second runs on a chip heated by the first)
+                for f in ((1, 0) if os.environ.get("ENC_PO_FIRST") == "1" else (0, 1)):
+                    res[(tag, kn, f)].append(t(L, ctxs[kn], kn, _native.EC_FLAG_PARITY_ONLY if f else 0))
     print("us per segment (min of 3 rounds), TB/s algorithmic; full | parity-only")
     for kn in CONFIGS:
         k, n = kn

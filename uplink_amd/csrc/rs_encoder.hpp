@@ -153,14 +153,27 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // on its own, is the limit: 8 + 4 waves once there are >= 32 parity rows
 // (DESIGN.md §4).
 constexpr int parity_compute_waves(int k, int n) { return n - k >= 32 ? 8 : 4; }
+// Few parity rows (<= 32) for many chunk inputs (>= 16): the loaders' share
+// of a tile (loads, data-piece stores, bit-slicing) is large next to the
+// compute, and 8 loader waves carrying half as many inputs each are faster
+// (RS(30,60) 6 %, RS(20,50) 3.5 %; with 40 or 51 parity rows 4 loaders stay
+// ahead: DESIGN.md §4 "Encode kernel").
+constexpr bool few_rows_many_inputs(int k, int n) { return n - k <= 32 && chunk_size(k) >= 16; }
 // Compute waves of the full encode: 4, one per SIMD beside a loader wave,
 // while a wave's rows fit its registers next to the loaders' (<= 13 rows:
 // RS(29,80) runs at 198 VGPRs, two waves per SIMD); more parity rows would
 // spill (RS(10,100) at 23 rows per wave: 120 B per lane to scratch), so
-// 8 compute waves then.
-constexpr int full_compute_waves(int k, int n) { return n - k > 52 ? 8 : 4; }
-// Workgroups per CU the LDS ring allows (one workgroup per CU above 80 KiB).
-constexpr int wgs_per_cu(int k) { return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 ? 2 : 1; }
+// 8 compute waves then.  A two-chunk tile with few rows and 8 loaders also
+// takes 8 (RS(50,80): 4 + 8 spills, 8 + 8 is 4 % faster than 4 + 4).
+constexpr int full_compute_waves(int k, int n) {
+    return n - k > 52 || (few_rows_many_inputs(k, n) && chunks_of(k) > 1) ? 8 : 4;
+}
+constexpr int full_loader_waves(int k, int n) { return few_rows_many_inputs(k, n) ? 8 : 4; }
+// Workgroups per CU: two when both LDS rings fit (<= 80 KiB each) and the
+// two workgroups' waves fit the CU's 16 slots of this occupancy.
+constexpr int wgs_per_cu(int k, int waves) {
+    return 2 * chunk_size(k) * 2048 * 2 <= 160 * 1024 && 2 * waves <= 16 ? 2 : 1;
+}
 
 }  // namespace enc
 }  // namespace uplink_ec

@@ -103,17 +103,17 @@ void join_compiles() {
         if (th.joinable()) th.join();
 }
 
-std::string variant_expr(int k, int n, int nc) {
+std::string variant_expr(int k, int n, int nc, int nl) {
     return "&uplink_ec::enc::rs_encode_special<" + std::to_string(k) + ", " + std::to_string(n) + ", " +
-           std::to_string(nc) + ", 4>";
+           std::to_string(nc) + ", " + std::to_string(nl) + ">";
 }
 
 // Compile (or read from the cache) the two variants of (k, n) for `arch`.
 void compile_entry(JitEntry *e, std::string arch, int k, int n) {
     std::lock_guard<std::mutex> serial(g_compile_mu);
     const std::string src = "#include \"rs_encoder.hpp\"\n";
-    const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n)),
-                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n));
+    const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n), enc::full_loader_waves(k, n)),
+                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n), 4);
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++20"};
     uint64_t h = 0xcbf29ce484222325ull;
     for (int i = 0; i < kJitHeaderCount; i++) h = fnv1a(h, kJitHeaderTexts[i], strlen(kJitHeaderTexts[i]));
@@ -247,9 +247,10 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
     ek->k = k;
     ek->n = n;
     ek->jit = true;
-    const int pnc = enc::parity_compute_waves(k, n), fnc = enc::full_compute_waves(k, n);
-    ek->full = {nullptr, f_full, (fnc + 4) * 64, enc::wgs_per_cu(k), "rs_encode_special (jit)"};
-    ek->parity = {nullptr, f_par, (pnc + 4) * 64, enc::wgs_per_cu(k), "rs_encode_special (jit, parity only)"};
+    const int pnc = enc::parity_compute_waves(k, n), fnc = enc::full_compute_waves(k, n),
+              fnl = enc::full_loader_waves(k, n);
+    ek->full = {nullptr, f_full, (fnc + fnl) * 64, enc::wgs_per_cu(k, fnc + fnl), "rs_encode_special (jit)"};
+    ek->parity = {nullptr, f_par, (pnc + 4) * 64, enc::wgs_per_cu(k, pnc + 4), "rs_encode_special (jit, parity only)"};
     EncoderKernel *out = ek.get();
     e->loaded[dev] = std::move(ek);
     return out;
