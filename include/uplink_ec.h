@@ -226,6 +226,21 @@ const char *ec_encode_kernel_name(const ec_ctx *ctx);
  * calls use the runtime-matrix kernel, with identical results.  Returns 1 when it is ready (with wait != 0:
  * after waiting for the compilation), 0 when this (k, n) has none. */
 int ec_prepare_encoder(const ec_ctx *ctx, int wait);
+/* Body of the runtime-matrix kernel for this ctx's decode (and other
+ * runtime-matrix) plans, DESIGN.md §4 "Straight-line rebuild":
+ *   EC_BODY_AUTO (default): the plan's generated straight-line code for
+ *     launches of at least 64 tiles (131,072 byte columns per share), the
+ *     jump table for smaller ones (per-stripe calls);
+ *   EC_BODY_JUMP_TABLE: always the jump table;
+ *   EC_BODY_STRAIGHT_LINE: generated code for every launch it fits.
+ * The results are identical.  No reference counterpart (an engine knob). */
+#define EC_BODY_AUTO 0
+#define EC_BODY_JUMP_TABLE 1
+#define EC_BODY_STRAIGHT_LINE 2
+int ec_set_body(ec_ctx *ctx, int body);
+/* which body the ctx's last runtime-matrix launch used: EC_BODY_JUMP_TABLE,
+ * EC_BODY_STRAIGHT_LINE, or EC_BODY_AUTO when there was none yet */
+int ec_last_body(const ec_ctx *ctx);
 
 #ifdef __cplusplus
 }

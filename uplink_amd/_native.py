@@ -29,6 +29,8 @@ EC_ERR_SHARE_SIZE = -13
 EC_ERR_AUTH = -14
 
 EC_FLAG_PARITY_ONLY = 0x1
+# ec_set_body: body of the runtime-matrix kernel (include/uplink_ec.h)
+EC_BODY_AUTO, EC_BODY_JUMP_TABLE, EC_BODY_STRAIGHT_LINE = 0, 1, 2
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 vp = ctypes.c_void_p
@@ -84,6 +86,8 @@ SIGNATURES = {
     "ec_set_device": (ctypes.c_int, [ctypes.c_int]),
     "ec_encode_kernel_name": (ctypes.c_char_p, [vp]),
     "ec_prepare_encoder": (ctypes.c_int, [vp, ctypes.c_int]),
+    "ec_set_body": (ctypes.c_int, [vp, ctypes.c_int]),
+    "ec_last_body": (ctypes.c_int, [vp]),
 }
 
 _lib = None

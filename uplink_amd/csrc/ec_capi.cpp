@@ -23,6 +23,7 @@
 #include "gf256.hpp"
 #include "rs_correct.hpp"
 #include "rs_kernels.hpp"
+#include "rs_sl.hpp"
 
 using namespace uplink_ec;
 
@@ -34,16 +35,27 @@ namespace {
 // (launch_jt_targets).  Plans are built once -- synchronously, on the
 // context's own setup stream -- and reused by every launch of that matrix, so
 // no launch allocates memory or prepares tables in stream order.
+//
+// Plans of at most kMaxOps rows can also carry the matrix as straight-line
+// code (rs_sl.hpp): a module made from the template code object on the first
+// launch that wants it, and the absolute addresses of its segments.
 struct MatPlan {
     std::vector<int> key;          // what the matrix is (decode: chosen share ids; see plan keys below)
     std::vector<int> missing;      // decode plans: the data positions rebuilt, in row order
     int rows = 0, nin = 0, coef_ld = 0;
     uint8_t *d_coef = nullptr;     // [j][r], ld = coef_ld
     std::vector<uint64_t *> d_tgt; // leaf addresses per block of kMaxOps rows
+    std::vector<uint8_t> M;        // rows x nin, row-major (for the straight-line code)
+    std::mutex sl_mu;
+    bool sl_tried = false;
+    hipModule_t sl_mod = nullptr;
+    uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
     ~MatPlan() {
         if (d_coef) (void)hipFree(d_coef);
         for (uint64_t *t : d_tgt)
             if (t) (void)hipFree(t);
+        if (d_sl) (void)hipFree(d_sl);
+        if (sl_mod) (void)hipModuleUnload(sl_mod);
     }
 };
 using PlanPtr = std::shared_ptr<MatPlan>;
@@ -113,6 +125,8 @@ struct ec_ctx {
     std::vector<std::unique_ptr<Workspace>> all_ws;
     std::deque<WsWaiter *> ws_waiters;  // callers waiting for a workspace, first come first served
     uint32_t *d_chk = nullptr;     // checked build: the kernels' violation word
+    int body = EC_BODY_AUTO;       // ec_set_body
+    int last_body = EC_BODY_AUTO;  // ec_last_body
     // EncodeSingle coalescing (group commit): callers queue; up to
     // kSingleLeaders of them at a time each run everything queued as one batch
     std::mutex single_mu;
@@ -229,6 +243,7 @@ int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int 
     p->key = std::move(key);
     p->rows = rows;
     p->nin = nin;
+    p->M.assign(M, M + (size_t)rows * nin);
     p->coef_ld = round16(std::max(rows, 1));
     std::vector<uint8_t> coef((size_t)nin * p->coef_ld + kCoefPad, 0);
     for (int r = 0; r < rows; r++)
@@ -342,10 +357,57 @@ int after_launch(uint32_t *chk, hipStream_t s) {
     return EC_OK;
 }
 
+// Launches of at least this many tiles use a plan's straight-line code under
+// EC_BODY_AUTO: its module costs a code generation and a module load once per
+// plan, which only pays over many stripes.
+constexpr int64_t kSlMinTiles = 64;
+
+// Make the plan's straight-line module (once; on failure the plan keeps
+// using the jump table).  Synchronous, on the context's setup stream.
+void ensure_sl(ec_ctx *c, MatPlan &plan) {
+    std::lock_guard<std::mutex> g(plan.sl_mu);
+    if (plan.sl_tried) return;
+    plan.sl_tried = true;
+    if (plan.rows < 1 || plan.rows > kMaxOps || plan.nin < 1 || plan.nin > kMaxOps) return;
+    size_t roff = 0;
+    std::vector<uint8_t> img = sl::template_image(&roff);
+    std::vector<uint32_t> code(sl::kRegionWords);
+    memcpy(code.data(), img.data() + roff, code.size() * 4);
+    std::vector<uint32_t> offs;
+    if (!sl::generate(plan.M.data(), plan.rows, plan.nin, code.data(), offs)) return;  // does not fit
+    memcpy(img.data() + roff, code.data(), code.size() * 4);
+    std::lock_guard<std::mutex> gs(c->setup_mu);
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    uint64_t *d = nullptr;
+    auto fail = [&](hipError_t e) {
+        hip_fail(e);
+        if (d) (void)hipFree(d);
+        if (mod) (void)hipModuleUnload(mod);
+    };
+    hipError_t e = hipModuleLoadData(&mod, img.data());
+    if (e == hipSuccess) e = hipModuleGetFunction(&fn, mod, "rs_sl_where");
+    if (e == hipSuccess) e = hipMalloc(&d, (offs.size() + 1) * sizeof(uint64_t));
+    if (e != hipSuccess) return fail(e);
+    void *args[] = {&d};
+    uint64_t base = 0;
+    e = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, c->setup, args, nullptr);
+    if (e == hipSuccess) e = hipMemcpyAsync(&base, d, sizeof(base), hipMemcpyDeviceToHost, c->setup);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->setup);
+    if (e != hipSuccess || base == 0) return fail(e == hipSuccess ? hipErrorInvalidValue : e);
+    std::vector<uint64_t> tab(offs.size());
+    for (size_t i = 0; i < offs.size(); i++) tab[i] = offs[i] == sl::kNoSegment ? 0 : base + offs[i];
+    e = hipMemcpyAsync(d, tab.data(), tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c->setup);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->setup);
+    if (e != hipSuccess) return fail(e);
+    plan.sl_mod = mod;
+    plan.d_sl = d;
+}
+
 // Launch the product described by `a` with the rows of `plan` (out_off gives
 // every row's offset; more than kMaxOps rows go in several launches, copies
 // in the first one only).
-int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, const MatPlan &plan, int64_t nseg, bool bitsliced,
+int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64_t nseg, bool bitsliced,
                hipStream_t s) {
     const int total_rows = plan.rows;
     int done = 0, blk = 0;
@@ -360,7 +422,15 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, const MatPlan &plan,
         if (done > 0)
             for (int j = 0; j < a.nin; j++) a.copy_off[j] = -1;
         set_extents(a, nseg, c->d_chk);
-        if (bitsliced) {
+        const bool want_sl = bitsliced && total_rows <= kMaxOps && c->body != EC_BODY_JUMP_TABLE &&
+                             (c->body == EC_BODY_STRAIGHT_LINE || a.total_tiles >= kSlMinTiles);
+        if (want_sl) ensure_sl(c, plan);
+        if (want_sl && plan.d_sl) {
+            a.jt_tgt = plan.d_sl;
+            c->last_body = EC_BODY_STRAIGHT_LINE;
+            HIP_TRY(launch_matmul_sl(a, 0, s));
+        } else if (bitsliced) {
+            c->last_body = EC_BODY_JUMP_TABLE;
             HIP_TRY(launch_matmul_generic(a, 0, s));
         } else {
             const int64_t keep = a.total_tiles;
@@ -454,6 +524,14 @@ int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const
 }  // namespace
 
 extern "C" {
+
+int ec_set_body(ec_ctx *c, int body) {
+    if (!c || body < EC_BODY_AUTO || body > EC_BODY_STRAIGHT_LINE) return EC_ERR_INVALID_ARG;
+    c->body = body;
+    return EC_OK;
+}
+
+int ec_last_body(const ec_ctx *c) { return c ? c->last_body : EC_BODY_AUTO; }
 
 int ec_device_count(void) {
     int n = 0;

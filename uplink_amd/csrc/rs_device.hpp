@@ -162,6 +162,25 @@ __device__ __forceinline__ void jt_inputs(u32x8 (&acc)[8], uint32_t xa, const ui
           "s67", "scc", "memory");
 }
 
+// The straight-line form (rs_sl.hpp): one call into the plan's generated
+// segment for this chunk, rows and wave; it reads the chunk's planes from LDS
+// at xa (pinned to v126), uses v[96:125] as scratch, adds into the
+// accumulators and returns through s[48:49].
+// `tp` points at the segment's address in the plan's table (a scalar load
+// inside the asm: the compiler would fetch it with a vector load).
+__device__ __forceinline__ void sl_segment(u32x8 (&acc)[8], uint32_t xa, const uint64_t *tp) {
+    asm volatile(
+        "s_load_dwordx2 s[52:53], %[tp], 0x0\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "s_swappc_b64 s[48:49], s[52:53]"
+        : "+{v[32:39]}"(acc[0]), "+{v[40:47]}"(acc[1]), "+{v[48:55]}"(acc[2]), "+{v[56:63]}"(acc[3]),
+          "+{v[64:71]}"(acc[4]), "+{v[72:79]}"(acc[5]), "+{v[80:87]}"(acc[6]), "+{v[88:95]}"(acc[7])
+        : [tp] "s"(tp), "{v126}"(xa)
+        : "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109",
+          "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",
+          "v123", "v124", "v125", "s48", "s49", "s52", "s53", "memory");
+}
+
 // Absolute address of leaf 0 of the jump table.  The table itself sits here,
 // behind a branch, in the code of the one kernel that calls this
 // (rs_jt_targets); the leaves are position-independent code that any kernel

@@ -62,9 +62,14 @@ __constant__ GfTables d_gf = make_gf_tables();
 // LDS size.
 constexpr int kJtRows = 8;  // accumulator rows per wave
 
-template <int NW>
+// SL: the straight-line form (rs_sl.hpp): instead of the jump table, each
+// wave calls the plan's generated code segment for (pass, chunk, row group)
+// once per chunk; a.jt_tgt then holds those segments' absolute addresses,
+// [pass][chunk][group].
+template <int NW, bool SL>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
+    const int nchunks = (a.nin + JC - 1) / JC;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *lds = smem;                                  // 2 x [JC][8 planes][64 lanes]
     const int lane = threadIdx.x & 63;
@@ -97,10 +102,14 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
                     const int j1 = j0 + JC;
                     load_inputs<NW, PER, true>(a, seg, c, wave, j1, a.nin - j1 < JC ? a.nin - j1 : JC, r);
                 }
-                if (cnt > 0)
-                    jt_inputs(acc, lds_addr + (uint32_t)(buf * JC * 8 * 64 * 4),
-                              a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
-                              (uint32_t)(OPW - cnt), (uint32_t)jn);
+                if (cnt > 0) {
+                    const uint32_t xa = lds_addr + (uint32_t)(buf * JC * 8 * 64 * 4);
+                    if constexpr (SL)
+                        sl_segment(acc, xa, a.jt_tgt + (pass * nchunks + j0 / JC) * NW + group);
+                    else
+                        jt_inputs(acc, xa, a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW,
+                                  (uint32_t)(NW * OPW * 8), (uint32_t)(OPW - cnt), (uint32_t)jn);
+                }
                 buf ^= 1;
             }
             uint32_t rows[OPW][8];
@@ -228,7 +237,8 @@ hipError_t launch_jt_targets(const RsArgs &a, uint64_t *targets, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
+template <bool SL>
+hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     if (!a.jt_tgt || a.nout > kMaxOps || a.nin > kMaxOps) return hipErrorInvalidValue;
     // up to 16 waves per CU (4 per SIMD: the jump-table body holds ~126
     // VGPRs); as few waves per workgroup as the rows need, since every wave
@@ -236,18 +246,22 @@ hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) {
     switch (jt_waves(a.nout)) {
     case 2:
         if (grid <= 0) grid = default_grid(a.total_tiles, 8);
-        hipLaunchKernelGGL((rs_matmul_jt<2>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);
+        hipLaunchKernelGGL((rs_matmul_jt<2, SL>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);
         break;
     case 3:
         if (grid <= 0) grid = default_grid(a.total_tiles, 5);
-        hipLaunchKernelGGL((rs_matmul_jt<3>), dim3(grid), dim3(3 * 64), jt_lds_bytes<3>(a), s, a);
+        hipLaunchKernelGGL((rs_matmul_jt<3, SL>), dim3(grid), dim3(3 * 64), jt_lds_bytes<3>(a), s, a);
         break;
     default:
         if (grid <= 0) grid = default_grid(a.total_tiles, 4);
-        hipLaunchKernelGGL((rs_matmul_jt<4>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
+        hipLaunchKernelGGL((rs_matmul_jt<4, SL>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
     }
     return hipGetLastError();
 }
+
+hipError_t launch_matmul_generic(const RsArgs &a, int grid, hipStream_t s) { return launch_matmul<false>(a, grid, s); }
+
+hipError_t launch_matmul_sl(const RsArgs &a, int grid, hipStream_t s) { return launch_matmul<true>(a, grid, s); }
 
 hipError_t launch_gather_shares(const uint8_t *stripes, const uint8_t *parity, const int *nums, int k, int64_t nreq,
                                int64_t bs, uint8_t *out, hipStream_t s) {

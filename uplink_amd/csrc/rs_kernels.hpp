@@ -42,6 +42,9 @@ hipError_t launch_encode_special(const EncoderKernel &e, const RsArgs &args, int
 // that matrix in args.jt_tgt (made by launch_jt_targets into
 // jt_targets_bytes(args) bytes of device memory; required).
 hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t stream);
+// The same kernel calling a plan's straight-line segments (rs_sl.hpp):
+// args.jt_tgt = their absolute addresses, [pass][chunk][group].
+hipError_t launch_matmul_sl(const RsArgs &args, int grid, hipStream_t stream);
 size_t jt_targets_bytes(const RsArgs &args);
 hipError_t launch_jt_targets(const RsArgs &args, uint64_t *targets, hipStream_t stream);
 // Byte-wise fallback (any ess, any alignment); coef as above.

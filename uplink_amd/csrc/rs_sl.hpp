@@ -1,0 +1,65 @@
+// Straight-line rebuild bodies: generated GF(2^8) multiply-accumulate code for
+// one runtime matrix (host side; rs_sl_codegen.cpp).
+//
+// The jump-table body (rs_device.hpp jt_inputs) multiplies a runtime
+// coefficient in with a call per (row, input) into a leaf, the accumulator row
+// chosen by VGPR index mode; both cost VALU issue (index mode
+// ~8 us, the calls ~4 us of an all-parity RS(29,80) rebuild).  For a matrix
+// that is used over many stripes (a decode plan) the library instead writes
+// the whole product as straight-line code: for each (pass, chunk of inputs,
+// wave row group) one code segment that reads the chunk's bit planes from
+// LDS, forms only the 4-plane combinations its coefficients use and applies
+// one v_bitop3 (or v_xor) per (row, plane, input) on fixed registers, i.e.
+// the compile-time encoder's body with the coefficients of this matrix.  The
+// segments go into the code region of a template code object
+// (rs_sl_region.hip), which is loaded as a module per plan; the
+// runtime-matrix kernel calls segment (pass, chunk, group) through a table
+// of absolute addresses, once per chunk.
+//
+// Register contract (shared with rs_matmul_jt<NW, true> in rs_kernels.hip and
+// with the jump table's layout): accumulators v[32:95] (row o, plane p at
+// v[32 + 8o + p]); lo[L] = v[95 + L], hi[H] = v[110 + H] (L, H = 1..15) as
+// scratch; v126 = LDS byte address of plane 0 of the chunk's first input for
+// this lane (input jj at +2048 jj, plane p at +256 p); return address s[48:49].
+// Generated code touches nothing else: no memory but LDS reads, no scalar
+// registers, no M0.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+// marker words at the start of the template's region, and its size
+#define UPLINK_SL_MAGIC0 0x5ec7a11e
+#define UPLINK_SL_MAGIC1 0x0b0d1e50
+#define UPLINK_SL_MAGIC2 0x2981e4c0
+#define UPLINK_SL_MAGIC3 0x7e91a7e5
+#define UPLINK_SL_REGION_WORDS 65536  // 256 KiB of code space per plan
+
+namespace uplink_ec {
+namespace sl {
+
+constexpr int kRegionWords = UPLINK_SL_REGION_WORDS;
+constexpr uint32_t kNoSegment = 0xffffffffu;
+
+// Row split of the runtime-matrix kernel (rs_kernels.hip): `rows` rows in
+// npass passes of at most nw * 8, each pass's rows dealt to the nw groups.
+struct Split {
+    int nw, npass;
+    int rbase(int pass, int g, int rows) const;
+    int count(int pass, int g, int rows) const;
+};
+Split split_for(int rows);  // the same wave count the kernel launch picks
+
+// Generate the segments of M (rows x nin, row-major) into `code` (kRegionWords
+// words, pre-filled by the caller).  seg_off receives, for [pass][chunk]
+// [group], the byte offset of that segment in the region (kNoSegment when the
+// group has no rows in that pass).  Returns the number of words used, or 0
+// when the code does not fit the region.
+size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector<uint32_t> &seg_off);
+
+// The template code object (an ELF) with its region restored (marker words +
+// s_endpgm fill); region_off receives the byte offset of the region in it.
+std::vector<uint8_t> template_image(size_t *region_off);
+
+}  // namespace sl
+}  // namespace uplink_ec

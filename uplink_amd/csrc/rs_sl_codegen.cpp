@@ -1,0 +1,168 @@
+// Straight-line rebuild bodies: code generation (see rs_sl.hpp for the design
+// and the register contract).
+//
+// Five gfx950 instruction forms are emitted, encoded here directly (each
+// encoding is checked against the LLVM disassembler and a CPU emulation of
+// the generated code in tests/test_sl_codegen.py):
+//   ds_read_b32    vD, v126 offset:O     plane p of input jj: O = 2048 jj + 256 p
+//   s_waitcnt      lgkmcnt(N)
+//   v_xor_b32_e32  vD, vA, vB            4-plane combinations; single-combination rows
+//   v_bitop3_b32   vD, vD, vL, vH 0x96   acc ^= lo[L] ^ hi[H]
+//   s_setpc_b64    s[48:49]              return to the calling kernel
+#include <string.h>
+
+#include "gf256_field.hpp"
+#include "rs_sl.hpp"
+#include "rs_sl_image.inc"
+
+namespace uplink_ec {
+namespace sl {
+
+namespace {
+
+constexpr int kAcc = 32, kLoBase = 95, kHiBase = 110, kXa = 126;
+constexpr int kRows = 8;  // accumulator rows per wave (rs_kernels.hip kJtRows)
+
+uint32_t lo_reg(int L) { return (uint32_t)(kLoBase + L); }
+uint32_t hi_reg(int H) { return (uint32_t)(kHiBase + H); }
+
+struct Emitter {
+    uint32_t *code;
+    size_t cap, n = 0;
+    bool overflow = false;
+    void word(uint32_t w) {
+        if (n < cap) code[n] = w;
+        else overflow = true;
+        n++;
+    }
+    void ds_read_b32(uint32_t vdst, uint32_t vaddr, uint32_t offset) {
+        word(0xd86c0000u | (offset & 0xffffu));
+        word((vdst << 24) | vaddr);
+    }
+    void waitcnt_lgkm(uint32_t cnt) { word(0xbf8cc07fu | ((cnt & 15u) << 8)); }
+    void v_xor(uint32_t vdst, uint32_t va, uint32_t vb) { word((0x15u << 25) | (vdst << 17) | (vb << 9) | (256u + va)); }
+    void v_bitop3_xor3(uint32_t vdst, uint32_t va, uint32_t vb, uint32_t vc) {
+        word(0xd2340200u | vdst);
+        word(0xd0000000u | ((256u + vc) << 18) | ((256u + vb) << 9) | (256u + va));
+    }
+    void s_setpc_ret() { word(0xbe801d30u); }
+};
+
+int low_bit(int m) { return m & -m; }
+
+// One segment: inputs j0 .. j0+jn-1 of the chunk into rows rbase .. rbase+cnt-1.
+void emit_segment(Emitter &e, const uint8_t *M, int nin, int rbase, int cnt, int j0, int jn) {
+    for (int jj = 0; jj < jn; jj++) {
+        const int j = j0 + jj;
+        bool need_lo[16] = {}, need_hi[16] = {};
+        bool any = false;
+        for (int o = 0; o < cnt; o++) {
+            const uint8_t c = M[(size_t)(rbase + o) * nin + j];
+            if (!c) continue;
+            for (int p = 0; p < 8; p++) {
+                const uint8_t row = mul_bitrow(c, p);
+                need_lo[row & 15] = true;
+                need_hi[row >> 4] = true;
+                any = true;
+            }
+        }
+        if (!any) continue;
+        // closure: lo[m] = lo[m ^ low(m)] ^ x[bit(low(m))]
+        for (int m = 15; m >= 1; m--) {
+            if (need_lo[m]) need_lo[m ^ low_bit(m)] = need_lo[low_bit(m)] = true;
+            if (need_hi[m]) need_hi[m ^ low_bit(m)] = need_hi[low_bit(m)] = true;
+        }
+        need_lo[0] = need_hi[0] = false;
+        const uint32_t base = (uint32_t)jj * 2048u;
+        int nhi = 0;
+        for (int q = 0; q < 4; q++)
+            if (need_lo[1 << q]) e.ds_read_b32(lo_reg(1 << q), kXa, base + 256u * q);
+        for (int q = 0; q < 4; q++)
+            if (need_hi[1 << q]) e.ds_read_b32(hi_reg(1 << q), kXa, base + 256u * (4 + q)), nhi++;
+        bool lo_combo = false, hi_combo = false;
+        for (int m = 1; m < 16; m++) {
+            if (m != low_bit(m)) lo_combo |= need_lo[m], hi_combo |= need_hi[m];
+        }
+        // the low planes land first (LDS returns in order): combine them while the high ones arrive
+        if (lo_combo) {
+            e.waitcnt_lgkm((uint32_t)nhi);
+            for (int m = 1; m < 16; m++)
+                if (need_lo[m] && m != low_bit(m)) e.v_xor(lo_reg(m), lo_reg(m ^ low_bit(m)), lo_reg(low_bit(m)));
+        }
+        e.waitcnt_lgkm(0);
+        if (hi_combo)
+            for (int m = 1; m < 16; m++)
+                if (need_hi[m] && m != low_bit(m)) e.v_xor(hi_reg(m), hi_reg(m ^ low_bit(m)), hi_reg(low_bit(m)));
+        for (int o = 0; o < cnt; o++) {
+            const uint8_t c = M[(size_t)(rbase + o) * nin + j];
+            if (!c) continue;
+            for (int p = 0; p < 8; p++) {
+                const uint8_t row = mul_bitrow(c, p);
+                const int L = row & 15, H = row >> 4;
+                const uint32_t acc = (uint32_t)(kAcc + kRows * o + p);
+                if (L && H) e.v_bitop3_xor3(acc, acc, lo_reg(L), hi_reg(H));
+                else if (L) e.v_xor(acc, acc, lo_reg(L));
+                else if (H) e.v_xor(acc, acc, hi_reg(H));
+            }
+        }
+    }
+    e.s_setpc_ret();
+}
+
+}  // namespace
+
+int Split::rbase(int pass, int g, int rows) const {
+    const int p0 = pass * rows / npass, prow = (pass + 1) * rows / npass - p0;
+    return p0 + g * prow / nw;
+}
+
+int Split::count(int pass, int g, int rows) const {
+    const int p0 = pass * rows / npass, prow = (pass + 1) * rows / npass - p0;
+    return p0 + (g + 1) * prow / nw - rbase(pass, g, rows);
+}
+
+Split split_for(int rows) {
+    Split s;
+    s.nw = rows <= 2 * kRows ? 2 : rows <= 3 * kRows ? 3 : 4;
+    s.npass = rows > 0 ? (rows + s.nw * kRows - 1) / (s.nw * kRows) : 1;
+    return s;
+}
+
+size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector<uint32_t> &seg_off) {
+    const Split sp = split_for(rows);
+    const int jc = 2 * sp.nw, nchunks = (nin + jc - 1) / jc;
+    seg_off.assign((size_t)sp.npass * nchunks * sp.nw, kNoSegment);
+    Emitter e{code, (size_t)kRegionWords};
+    // the region's first 64 words stay s_endpgm: no segment starts at offset 0
+    e.n = 64;
+    for (int pass = 0; pass < sp.npass; pass++)
+        for (int ch = 0; ch < nchunks; ch++)
+            for (int g = 0; g < sp.nw; g++) {
+                const int cnt = sp.count(pass, g, rows);
+                if (cnt <= 0) continue;
+                // segments start on 64-byte instruction-cache lines
+                while (e.n & 15) e.word(0xbf810000u);
+                seg_off[((size_t)pass * nchunks + ch) * sp.nw + g] = (uint32_t)(e.n * 4);
+                const int j0 = ch * jc, jn = nin - j0 < jc ? nin - j0 : jc;
+                emit_segment(e, M, nin, sp.rbase(pass, g, rows), cnt, j0, jn);
+            }
+    if (e.overflow) return 0;
+    return e.n;
+}
+
+std::vector<uint8_t> template_image(size_t *region_off) {
+    std::vector<uint8_t> img(sizeof(kSlHead) + (size_t)kRegionWords * 4 + sizeof(kSlTail));
+    memcpy(img.data(), kSlHead, sizeof(kSlHead));
+    uint32_t *r = (uint32_t *)(img.data() + sizeof(kSlHead));
+    const uint32_t magic[4] = {UPLINK_SL_MAGIC0, UPLINK_SL_MAGIC1, UPLINK_SL_MAGIC2, UPLINK_SL_MAGIC3};
+    for (int i = 0; i < kRegionWords; i++) {
+        const uint32_t w = i < 4 ? magic[i] : 0xbf810000u;
+        memcpy((uint8_t *)r + 4 * (size_t)i, &w, 4);
+    }
+    memcpy(img.data() + sizeof(kSlHead) + (size_t)kRegionWords * 4, kSlTail, sizeof(kSlTail));
+    *region_off = sizeof(kSlHead);
+    return img;
+}
+
+}  // namespace sl
+}  // namespace uplink_ec
