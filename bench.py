@@ -438,7 +438,10 @@ def main():
     kernels = {
         "encode": {"kernel": f"rs_encode_special<29,80,4,4> ({enc_name})", "avg_us": round(t_enc_full * 1e6, 2),
                    "bytes_per_launch": int(enc_bytes), "achieved_GBps": round(enc_gbps, 1)},
-        "decode": {"kernel": "rs_matmul_jt<NW>", "avg_us": round(t_dec_full * 1e6, 2),
+        "decode": {"kernel": ("rs_matmul_jt<NW, true> (straight-line body)"
+                              if L.ec_last_body(ctx) == _native.EC_BODY_STRAIGHT_LINE
+                              else "rs_matmul_jt<NW, false> (jump-table body)"),
+                   "avg_us": round(t_dec_full * 1e6, 2),
                    "bytes_per_launch": int(dec_bytes), "achieved_GBps": round(dec_gbps, 1),
                    "us_per_segment_by_set": {
                        f"set{i}:m={K - sum(1 for x in sets[i] if x < K)}": round(sum(v) / len(v), 2)

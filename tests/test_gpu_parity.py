@@ -106,10 +106,13 @@ def test_full_size_rs_29_80_64mib(oracle):
     d_pieces = gpu_encode(sch, seg)
     ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=min(os.cpu_count() or 1, 16))
     assert np.array_equal(d_pieces.cpu().numpy()[0], ref)
-    for nums in (list(range(51, 80)), sorted(np.random.default_rng(29).choice(80, 29, replace=False).tolist())):
-        out = gpu_rebuild(sch, d_pieces, nums, 9040)[0]
-        assert np.array_equal(out, seg)
-        assert eestream.unpad(out.tobytes()) == raw.tobytes()
+    for body in (_native.EC_BODY_AUTO, _native.EC_BODY_JUMP_TABLE):
+        assert sch._lib.ec_set_body(sch._ctx, body) == 0
+        for nums in (list(range(51, 80)), sorted(np.random.default_rng(29).choice(80, 29, replace=False).tolist())):
+            out = gpu_rebuild(sch, d_pieces, nums, 9040)[0]
+            assert np.array_equal(out, seg)
+            assert eestream.unpad(out.tobytes()) == raw.tobytes()
+            assert sch._lib.ec_last_body(sch._ctx) == (body or _native.EC_BODY_STRAIGHT_LINE)
 
 
 def test_full_size_rs_20_60_ess4096(oracle):
@@ -506,14 +509,20 @@ def test_unsafe_rs_scheme_decode_is_rebuild(oracle):
     assert np.array_equal(safe.decode(None, bad), stripe)
 
 
+BODIES = [pytest.param(_native.EC_BODY_JUMP_TABLE, id="jt"), pytest.param(_native.EC_BODY_STRAIGHT_LINE, id="sl")]
+
+
+@pytest.mark.parametrize("body", BODIES)
 @pytest.mark.parametrize("k,n", [(29, 80), (20, 60), (50, 80)])
-def test_rebuild_every_missing_count(oracle, k, n):
+def test_rebuild_every_missing_count(oracle, k, n, body):
     """Rebuild with every number m of missing data shares, 0..min(k, n-k):
     this walks every rebuild kernel width (2, 3 or 4 waves of up to 8 rows,
     several passes beyond 32 rows), every right-aligned entry point into the
-    call sequence, and the copy-only case m = 0."""
+    call sequence, and the copy-only case m = 0 -- through the jump table and
+    through each plan's generated straight-line code."""
     ess, stripes = 256, 40
     sch = scheme(k, n, ess)
+    assert sch._lib.ec_set_body(sch._ctx, body) == 0
     rng = np.random.default_rng(k * 1000 + n)
     seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
     d_pieces = gpu_encode(sch, seg)
@@ -522,6 +531,43 @@ def test_rebuild_every_missing_count(oracle, k, n):
         parity = sorted(rng.choice(np.arange(k, n), m, replace=False).tolist())
         nums = data + parity
         assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), m
+        if m > 0:
+            assert sch._lib.ec_last_body(sch._ctx) == body
+
+
+@pytest.mark.parametrize("k,n,ess,stripes", [c for c in CONFIGS if c[2] % 16 == 0])
+def test_straight_line_body_vs_oracle(oracle, k, n, ess, stripes):
+    """Every bit-sliced configuration with the straight-line body forced:
+    rebuilds from three share sets, and the encode of the (k, n) without a
+    compile-time encoder (RS(64,96), RS(128,256): their parity plans, up to 128
+    rows, run as generated code too), bit-exact against the oracle."""
+    rng = np.random.default_rng(k * 7 + n + ess)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=4)
+    assert np.array_equal(gpu_encode(sch, seg).cpu().numpy()[0], ref)
+    d_pieces = torch.from_numpy(np.ascontiguousarray(ref)).cuda().reshape(1, n, -1)
+    for nums in (list(range(n - k, n)), sorted(rng.choice(n, k, replace=False).tolist())):
+        assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), nums
+        if any(x >= k for x in nums) and k <= 64:  # RS(128,256)'s plans exceed the 256-KiB code region
+            assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
+
+
+def test_auto_body_uses_straight_line_for_segments(oracle):
+    """EC_BODY_AUTO: a whole segment's rebuild runs the plan's generated code,
+    a per-stripe call the jump table; both bit-exact."""
+    k, n, ess, stripes = 29, 80, 256, 600  # 75 tiles of 2048 columns (the threshold is 64)
+    rng = np.random.default_rng(77)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    d_pieces = gpu_encode(sch, seg)
+    nums = list(range(n - k, n))
+    assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg)
+    assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
+    assert np.array_equal(gpu_rebuild(sch, d_pieces[:, :, :ess].contiguous(), nums, 1)[0], seg[:k * ess])
+    assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_JUMP_TABLE
+    assert sch._lib.ec_set_body(sch._ctx, 3) == _native.EC_ERR_INVALID_ARG
 
 
 @pytest.mark.parametrize("extra,bad,scatter", [(2, 1, 0), (4, 1, 0), (4, 2, 0), (6, 2, 40), (8, 3, 200), (4, 3, 0)])
