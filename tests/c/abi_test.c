@@ -45,11 +45,14 @@ static void fill(uint8_t *p, size_t n) {
     for (size_t i = 0; i < n; i++) p[i] = rnd8();
 }
 
-static void scheme_surface(int k, int n, int ess) {
+/* body: EC_BODY_AUTO (per-stripe calls on the jump table) or
+ * EC_BODY_STRAIGHT_LINE (every runtime-matrix launch on generated code) */
+static void scheme_surface(int k, int n, int ess, int body) {
     ec_ctx *ctx = NULL;
     int rc = ec_create(k, n, ess, &ctx);
     CHECK(rc == EC_OK, "ec_create(%d,%d,%d) = %d (%s)", k, n, ess, rc, ec_strerror(rc));
     if (rc) return;
+    CHECK(ec_set_body(ctx, body) == EC_OK, "ec_set_body(%d)", body);
     CHECK(ec_required(ctx) == k && ec_total(ctx) == n && ec_share_size(ctx) == ess &&
               ec_stripe_size(ctx) == k * ess,
           "sizes");
@@ -94,6 +97,9 @@ static void scheme_surface(int k, int n, int ess) {
     }
     CHECK(ec_rebuild(ctx, k, nums, shp, ess, out) == EC_OK, "ec_rebuild");
     CHECK(memcmp(out, in, stripe) == 0, "ec_rebuild != input (%d,%d,%d)", k, n, ess);
+    if (ess % 16 == 0)
+        CHECK(ec_last_body(ctx) == (body == EC_BODY_STRAIGHT_LINE ? EC_BODY_STRAIGHT_LINE : EC_BODY_JUMP_TABLE),
+              "body of a per-stripe rebuild: %d", ec_last_body(ctx));
     if (n - k >= 2) {
         /* Decode with 2 extra shares, one of them corrupted: Berlekamp-Welch */
         int ns = k + 2;
@@ -190,8 +196,10 @@ int main(void) {
     CHECK(ec_device_count() >= 1, "no device");
     const int cfg[][3] = {{2, 4, 1024}, {4, 10, 256}, {29, 80, 256}, {20, 60, 4096}, {3, 7, 100}, {10, 20, 64}};
     for (size_t i = 0; i < sizeof cfg / sizeof cfg[0]; i++) {
-        printf("RS(%d,%d) ess %d\n", cfg[i][0], cfg[i][1], cfg[i][2]);
-        scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2]);
+        for (int body = EC_BODY_AUTO; body <= EC_BODY_STRAIGHT_LINE; body += EC_BODY_STRAIGHT_LINE) {
+            printf("RS(%d,%d) ess %d body %d\n", cfg[i][0], cfg[i][1], cfg[i][2], body);
+            scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2], body);
+        }
     }
     printf("adjacent stages\n");
     adjacent_stages();

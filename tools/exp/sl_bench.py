@@ -9,7 +9,7 @@
    outputs compared with the segments; the time the first straight-line launch
    of a plan takes (code generation + module load + launch).
 3. The reference benchmark configurations' all-parity rebuilds.
-python tools/exp/sl_bench.py [--small-only]
+python tools/exp/sl_bench.py [--small-only | --k29-only]
 """
 import ctypes
 import json
@@ -97,6 +97,8 @@ def main():
     if "--small-only" in sys.argv:
         return
     run(L, 29, 80, 16, 64 << 20, s)
+    if "--k29-only" in sys.argv:
+        return
     for k, n in ((20, 50), (30, 60), (50, 80)):
         r = run(L, k, n, 8, 64 << 20, s)
         del r

@@ -51,6 +51,9 @@ struct MatPlan {
     hipModule_t sl_mod = nullptr;
     uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
     ~MatPlan() {
+        // a launch that used this plan may still be in flight (its last
+        // reference can go while a caller's stream runs it)
+        if (sl_mod) (void)hipDeviceSynchronize();
         if (d_coef) (void)hipFree(d_coef);
         for (uint64_t *t : d_tgt)
             if (t) (void)hipFree(t);
