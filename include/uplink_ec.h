@@ -215,10 +215,13 @@ int ec_gcm_open_host(const uint8_t key[32], const uint8_t nonce[12], const uint8
 /* ---- device helpers ---- */
 int ec_device_count(void);
 int ec_set_device(int device);
-/* name of the kernel ec_encode_segments uses for this ctx right now:
- * "special" (compile-time G, built into the library), "special-jit" (compiled
- * for this (k, n) at run time), "generic" (runtime matrix), "bytes" (ess not a
- * multiple of 16) or "copy" (n == k) */
+/* name of the kernel ec_encode_segments uses for whole segments of this ctx
+ * right now: "straight-line" (at most 32 parity rows: the runtime-matrix
+ * kernel with the parity rows as generated straight-line code, unless
+ * ec_set_body selected the jump table), "special" (compile-time G, built into
+ * the library), "special-jit" (compiled for this (k, n) at run time),
+ * "generic" (runtime matrix), "bytes" (ess not a multiple of 16) or "copy"
+ * (n == k) */
 const char *ec_encode_kernel_name(const ec_ctx *ctx);
 /* The compile-time-G encoder of a (k, n) that is not built into the library
  * is compiled in the background from its first encode call (or this call) on

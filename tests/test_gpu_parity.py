@@ -619,12 +619,16 @@ def test_reference_bench_configs_use_library_encoders(oracle, k, n):
     ess = 256
     stripes = (8 << 20) // (k * ess)
     sch = scheme(k, n, ess)
-    assert _kernel_name(sch) == "special"
     rng = np.random.default_rng(k * 131 + n)
     seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
     ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
-    assert np.array_equal(gpu_encode(sch, seg).cpu().numpy()[0], ref)
-    assert np.array_equal(gpu_encode(sch, seg, parity_only=True).cpu().numpy()[0], ref[k:])
+    # default: at most 32 parity rows run on the parity plan's straight-line code; with the
+    # jump-table body selected, on the library-built compile-time encoder
+    for body, name in ((_native.EC_BODY_AUTO, "straight-line"), (_native.EC_BODY_JUMP_TABLE, "special")):
+        assert sch._lib.ec_set_body(sch._ctx, body) == 0
+        assert _kernel_name(sch) == name
+        assert np.array_equal(gpu_encode(sch, seg).cpu().numpy()[0], ref)
+        assert np.array_equal(gpu_encode(sch, seg, parity_only=True).cpu().numpy()[0], ref[k:])
 
 
 @pytest.mark.parametrize("k,n,stripes", [(5, 9, 33), (37, 50, 17), (10, 20, 1025), (3, 70, 40), (36, 40, 9),
@@ -639,6 +643,9 @@ def test_run_time_compiled_encoder(oracle, k, n, stripes):
     runtime-matrix kernel (test_encode_rebuild_vs_oracle covers that path)."""
     ess = 256
     sch = scheme(k, n, ess)
+    # the compiled encoder runs for few parity rows only with the jump-table body selected
+    # (otherwise the parity plan's straight-line code does; both checked below)
+    assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_JUMP_TABLE) == 0
     assert sch._lib.ec_prepare_encoder(sch._ctx, 1) == 1
     assert _kernel_name(sch) == "special-jit"
     rng = np.random.default_rng(k * 7 + n)
@@ -647,11 +654,15 @@ def test_run_time_compiled_encoder(oracle, k, n, stripes):
     f = oracle.FEC(k, n)
     refs = [f.encode_segment(seg[i * stripes * k * ess:(i + 1) * stripes * k * ess], ess, threads=8)
             for i in range(nseg)]
-    got = gpu_encode(sch, seg, nseg=nseg).cpu().numpy()
-    par = gpu_encode(sch, seg, nseg=nseg, parity_only=True).cpu().numpy()
-    for i in range(nseg):
-        assert np.array_equal(got[i], refs[i]), i
-        assert np.array_equal(par[i], refs[i][k:]), i
+    for body in (_native.EC_BODY_JUMP_TABLE, _native.EC_BODY_STRAIGHT_LINE):
+        assert sch._lib.ec_set_body(sch._ctx, body) == 0
+        if body == _native.EC_BODY_STRAIGHT_LINE:
+            assert _kernel_name(sch) == ("straight-line" if n - k <= 32 else "special-jit")
+        got = gpu_encode(sch, seg, nseg=nseg).cpu().numpy()
+        par = gpu_encode(sch, seg, nseg=nseg, parity_only=True).cpu().numpy()
+        for i in range(nseg):
+            assert np.array_equal(got[i], refs[i]), (body, i)
+            assert np.array_equal(par[i], refs[i][k:]), (body, i)
 
 
 def test_prepare_encoder_reports_limits():
@@ -662,6 +673,8 @@ def test_prepare_encoder_reports_limits():
     # k > 48: the two-chunk compiled body is no faster than the runtime-matrix kernel there
     s3 = scheme(60, 80, 256)
     assert s3._lib.ec_prepare_encoder(s3._ctx, 0) == 0
+    assert _kernel_name(s3) == "straight-line"  # 20 parity rows
+    assert s3._lib.ec_set_body(s3._ctx, _native.EC_BODY_JUMP_TABLE) == 0
     assert _kernel_name(s3) == "generic"
     s2 = scheme(29, 80, 256)
     assert s2._lib.ec_prepare_encoder(s2._ctx, 0) == 1

@@ -365,6 +365,19 @@ int after_launch(uint32_t *chk, hipStream_t s) {
 // plan, which only pays over many stripes.
 constexpr int64_t kSlMinTiles = 64;
 
+// Whole-segment encodes with at most this many parity rows run on the
+// parity plan's straight-line code instead of a compile-time encoder: one
+// pass of the runtime-matrix kernel (up to 4 waves of 8 rows), 16 waves per
+// CU that all load and compute, measured equal or faster for RS(20,50),
+// (30,60), (50,80) (parity-only 3-17 % faster); with 40 and 51 parity rows
+// (RS(20,60), RS(29,80)) the compile-time encoder stays ahead.
+constexpr int kSlEncodeMaxRows = 32;
+
+bool sl_encoder(const ec_ctx *c) {
+    return c->ess % 16 == 0 && c->n > c->k && c->n - c->k <= kSlEncodeMaxRows && c->k <= kMaxOps &&
+           c->body != EC_BODY_JUMP_TABLE;
+}
+
 // Make the plan's straight-line module (once; on failure the plan keeps
 // using the jump table).  Synchronous, on the context's setup stream.
 void ensure_sl(ec_ctx *c, MatPlan &plan) {
@@ -645,6 +658,7 @@ const char *ec_encode_kernel_name(const ec_ctx *c) {
     if (!c) return "";
     if (c->ess % 16) return "bytes";
     if (c->n == c->k) return "copy";
+    if (sl_encoder(c)) return "straight-line";
     DeviceGuard dg(c->device);
     const EncoderKernel *e = find_encoder(c->k, c->n);
     return e ? (e->jit ? "special-jit" : "special") : "generic";
@@ -692,7 +706,10 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
     if (n == k) {  // replication of the data only: copies, no parity rows
         if (parity_only) return EC_OK;
     } else if (bits) {
-        const EncoderKernel *ek = find_encoder(c->k, c->n);
+        // few parity rows: the runtime-matrix kernel with the parity plan's
+        // straight-line code (run_matmul picks it for launches this large)
+        const bool sl = sl_encoder(c) && (c->body == EC_BODY_STRAIGHT_LINE || a.total_tiles >= kSlMinTiles);
+        const EncoderKernel *ek = sl ? nullptr : find_encoder(c->k, c->n);
         if (ek) {
             a.coef = nullptr;
             set_extents(a, (int64_t)nseg, c->d_chk);

@@ -40,6 +40,7 @@
 #include "gf256_field.hpp"
 #include "rs_device.hpp"
 #include "rs_kernels.hpp"
+#include "rs_sl.hpp"
 
 namespace uplink_ec {
 namespace {
@@ -243,7 +244,23 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     // up to 16 waves per CU (4 per SIMD: the jump-table body holds ~126
     // VGPRs); as few waves per workgroup as the rows need, since every wave
     // rebuilds the 4-plane combinations of each input for its own rows
-    switch (jt_waves(a.nout)) {
+    switch (SL ? sl::split_for(a.nout).nw : jt_waves(a.nout)) {
+    case 8:
+        if (grid <= 0) grid = default_grid(a.total_tiles, 2);
+        hipLaunchKernelGGL((rs_matmul_jt<8, true>), dim3(grid), dim3(8 * 64), jt_lds_bytes<8>(a), s, a);
+        break;
+    case 7:
+        if (grid <= 0) grid = default_grid(a.total_tiles, 2);
+        hipLaunchKernelGGL((rs_matmul_jt<7, true>), dim3(grid), dim3(7 * 64), jt_lds_bytes<7>(a), s, a);
+        break;
+    case 6:
+        if (grid <= 0) grid = default_grid(a.total_tiles, 2);
+        hipLaunchKernelGGL((rs_matmul_jt<6, true>), dim3(grid), dim3(6 * 64), jt_lds_bytes<6>(a), s, a);
+        break;
+    case 5:
+        if (grid <= 0) grid = default_grid(a.total_tiles, 3);
+        hipLaunchKernelGGL((rs_matmul_jt<5, true>), dim3(grid), dim3(5 * 64), jt_lds_bytes<5>(a), s, a);
+        break;
     case 2:
         if (grid <= 0) grid = default_grid(a.total_tiles, 8);
         hipLaunchKernelGGL((rs_matmul_jt<2, SL>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);

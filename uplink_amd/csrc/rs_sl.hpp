@@ -41,14 +41,15 @@ namespace sl {
 constexpr int kRegionWords = UPLINK_SL_REGION_WORDS;
 constexpr uint32_t kNoSegment = 0xffffffffu;
 
-// Row split of the runtime-matrix kernel (rs_kernels.hip): `rows` rows in
-// npass passes of at most nw * 8, each pass's rows dealt to the nw groups.
+// Row split of the runtime-matrix kernel (rs_kernels.hip) with a
+// straight-line body: `rows` rows in npass passes of at most nw * 8, each
+// pass's rows dealt to the nw groups (waves).
 struct Split {
     int nw, npass;
     int rbase(int pass, int g, int rows) const;
     int count(int pass, int g, int rows) const;
 };
-Split split_for(int rows);  // the same wave count the kernel launch picks
+Split split_for(int rows);  // the kernel launch (launch_matmul_sl) uses the same split
 
 // Generate the segments of M (rows x nin, row-major) into `code` (kRegionWords
 // words, pre-filled by the caller).  seg_off receives, for [pass][chunk]

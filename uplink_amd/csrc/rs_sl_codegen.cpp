@@ -123,7 +123,9 @@ int Split::count(int pass, int g, int rows) const {
 
 Split split_for(int rows) {
     Split s;
-    s.nw = rows <= 2 * kRows ? 2 : rows <= 3 * kRows ? 3 : 4;
+    // 2-4 waves as the jump table; past 32 rows up to 8 waves (2 workgroups
+    // per CU), so up to 64 rows take one pass over the inputs
+    s.nw = rows <= 2 * kRows ? 2 : rows <= 3 * kRows ? 3 : rows >= 8 * kRows ? 8 : (rows + kRows - 1) / kRows;
     s.npass = rows > 0 ? (rows + s.nw * kRows - 1) / (s.nw * kRows) : 1;
     return s;
 }
