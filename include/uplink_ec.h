@@ -235,7 +235,8 @@ int ec_prepare_encoder(const ec_ctx *ctx, int wait);
  *     launches of at least 64 tiles (131,072 byte columns per share), the
  *     jump table for smaller ones (per-stripe calls);
  *   EC_BODY_JUMP_TABLE: always the jump table;
- *   EC_BODY_STRAIGHT_LINE: generated code for every launch it fits.
+ *   EC_BODY_STRAIGHT_LINE: generated code for every launch it fits, and
+ *     every encode on it (also those a compile-time encoder would take).
  * The results are identical.  No reference counterpart (an engine knob). */
 #define EC_BODY_AUTO 0
 #define EC_BODY_JUMP_TABLE 1

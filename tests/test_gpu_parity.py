@@ -657,7 +657,7 @@ def test_run_time_compiled_encoder(oracle, k, n, stripes):
     for body in (_native.EC_BODY_JUMP_TABLE, _native.EC_BODY_STRAIGHT_LINE):
         assert sch._lib.ec_set_body(sch._ctx, body) == 0
         if body == _native.EC_BODY_STRAIGHT_LINE:
-            assert _kernel_name(sch) == ("straight-line" if n - k <= 32 else "special-jit")
+            assert _kernel_name(sch) == "straight-line"
         got = gpu_encode(sch, seg, nseg=nseg).cpu().numpy()
         par = gpu_encode(sch, seg, nseg=nseg, parity_only=True).cpu().numpy()
         for i in range(nseg):

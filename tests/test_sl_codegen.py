@@ -152,12 +152,12 @@ def check_matrix(M, seed):
     nw, npass, nchunks, offs, words = generate(M)
     assert len(offs) == npass * nchunks * nw
     assert len(words) <= 65536
-    jc = 2 * nw
+    chs = -(-nin // nchunks)  # chunks dealt evenly (rs_kernels.hip)
     for pass_ in range(npass):
         p0 = pass_ * rows // npass
         prow = (pass_ + 1) * rows // npass - p0
         for ch in range(nchunks):
-            j0, jn = ch * jc, min(jc, nin - ch * jc)
+            j0, jn = ch * chs, min(chs, nin - ch * chs)
             x = rng.integers(0, 256, (jn, 32), dtype=np.uint8)
             lds = {}
             for jj in range(jn):

@@ -1,13 +1,12 @@
 #!/usr/bin/env python3
 """Experiment (GPU box): the encode through the runtime-matrix kernel with
-straight-line code (5-8 waves per workgroup, one pass for up to 64 parity
-rows) against the compile-time encoder, full and parity-only, 16 x 64 MiB
-segments.  Runs itself twice, with and without UPLINK_EXP_GENERIC_ENCODE.
-python tools/exp/sl_encode_probe.py"""
+straight-line code (ec_set_body(EC_BODY_STRAIGHT_LINE): 5-8 waves per
+workgroup, one pass for up to 64 parity rows) against the compile-time
+encoder (EC_BODY_JUMP_TABLE), full and parity-only, 16 x 64 MiB segments.
+python tools/exp/sl_encode_probe.py [k n ...]"""
 import ctypes
 import json
 import os
-import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -17,7 +16,7 @@ sys.path.insert(0, ROOT)
 CONFIGS = ((29, 80), (20, 50), (30, 60), (50, 80), (20, 60))
 
 
-def child():
+def child(configs):
     import numpy as np
     import torch
     from oracle import oracle as O
@@ -25,13 +24,14 @@ def child():
     L = _native.load()
     s = torch.cuda.current_stream().cuda_stream
     nseg, ess = 16, 256
-    for k, n in CONFIGS:
+    for (k, n), body in [(c, b) for c in configs for b in (_native.EC_BODY_JUMP_TABLE, _native.EC_BODY_STRAIGHT_LINE)]:
         stripes = ((64 << 20) + 4 + k * ess - 1) // (k * ess)
         spad, plen = stripes * k * ess, stripes * ess
         ctx = ctypes.c_void_p()
         assert L.ec_create(k, n, ess, ctypes.byref(ctx)) == 0
+        assert L.ec_set_body(ctx, body) == 0
         segs = torch.randint(0, 256, (nseg, spad), dtype=torch.uint8, device="cuda")
-        res = {"k": k, "n": n, "generic": "UPLINK_EXP_GENERIC_ENCODE" in os.environ}
+        res = {"k": k, "n": n, "kernel": L.ec_encode_kernel_name(ctx).decode()}
         for name, flags, rows in (("full", 0, n), ("parity", _native.EC_FLAG_PARITY_ONLY, n - k)):
             pcs = torch.empty((nseg, rows, plen), dtype=torch.uint8, device="cuda")
 
@@ -59,17 +59,5 @@ def child():
 
 
 if __name__ == "__main__":
-    if "--child" in sys.argv:
-        child()
-    else:
-        for generic in (False, True):
-            env = dict(os.environ)
-            env.pop("UPLINK_EXP_GENERIC_ENCODE", None)
-            if generic:
-                env["UPLINK_EXP_GENERIC_ENCODE"] = "1"
-            r = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
-                               timeout=300)
-            sys.stdout.write(r.stdout)
-            if r.returncode:
-                sys.stdout.write(r.stderr[-2000:])
-                sys.exit(r.returncode)
+    a = [int(x) for x in sys.argv[1:]]
+    child(list(zip(a[0::2], a[1::2])) or CONFIGS)

@@ -373,9 +373,10 @@ constexpr int64_t kSlMinTiles = 64;
 // (RS(20,60), RS(29,80)) the compile-time encoder stays ahead.
 constexpr int kSlEncodeMaxRows = 32;
 
+// (EC_BODY_STRAIGHT_LINE: every encode the runtime-matrix kernel takes.)
 bool sl_encoder(const ec_ctx *c) {
-    return c->ess % 16 == 0 && c->n > c->k && c->n - c->k <= kSlEncodeMaxRows && c->k <= kMaxOps &&
-           c->body != EC_BODY_JUMP_TABLE;
+    return c->ess % 16 == 0 && c->n > c->k && c->k <= kMaxOps && c->n - c->k <= kMaxOps &&
+           (c->body == EC_BODY_STRAIGHT_LINE || (c->body == EC_BODY_AUTO && c->n - c->k <= kSlEncodeMaxRows));
 }
 
 // Make the plan's straight-line module (once; on failure the plan keeps

@@ -70,7 +70,10 @@ constexpr int kJtRows = 8;  // accumulator rows per wave
 template <int NW, bool SL>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
+    // the inputs in as few chunks of at most JC as they need, dealt evenly
+    // (29 inputs on 7 waves: 10 + 10 + 9, not 14 + 14 + 1)
     const int nchunks = (a.nin + JC - 1) / JC;
+    const int CH = (a.nin + nchunks - 1) / nchunks;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *lds = smem;                                  // 2 x [JC][8 planes][64 lanes]
     const int lane = threadIdx.x & 63;
@@ -93,20 +96,20 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 #pragma unroll
             for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
             StageRegs<PER> r;
-            load_inputs<NW, PER, true>(a, seg, c, wave, 0, a.nin < JC ? a.nin : JC, r);
-            for (int j0 = 0; j0 < a.nin; j0 += JC) {
-                const int jn = a.nin - j0 < JC ? a.nin - j0 : JC;
+            load_inputs<NW, PER, true>(a, seg, c, wave, 0, a.nin < CH ? a.nin : CH, r);
+            for (int j0 = 0; j0 < a.nin; j0 += CH) {
+                const int jn = a.nin - j0 < CH ? a.nin - j0 : CH;
                 slice_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
                 lds_barrier();
                 // the next chunk's loads are in flight while this chunk is multiplied in
-                if (j0 + JC < a.nin) {
-                    const int j1 = j0 + JC;
-                    load_inputs<NW, PER, true>(a, seg, c, wave, j1, a.nin - j1 < JC ? a.nin - j1 : JC, r);
+                if (j0 + CH < a.nin) {
+                    const int j1 = j0 + CH;
+                    load_inputs<NW, PER, true>(a, seg, c, wave, j1, a.nin - j1 < CH ? a.nin - j1 : CH, r);
                 }
                 if (cnt > 0) {
                     const uint32_t xa = lds_addr + (uint32_t)(buf * JC * 8 * 64 * 4);
                     if constexpr (SL)
-                        sl_segment(acc, xa, a.jt_tgt + (pass * nchunks + j0 / JC) * NW + group);
+                        sl_segment(acc, xa, a.jt_tgt + (pass * nchunks + j0 / CH) * NW + group);
                     else
                         jt_inputs(acc, xa, a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW,
                                   (uint32_t)(NW * OPW * 8), (uint32_t)(OPW - cnt), (uint32_t)jn);

@@ -21,6 +21,8 @@
 // v[32 + 8o + p]); lo[L] = v[95 + L], hi[H] = v[110 + H] (L, H = 1..15) as
 // scratch; v126 = LDS byte address of plane 0 of the chunk's first input for
 // this lane (input jj at +2048 jj, plane p at +256 p); return address s[48:49].
+// A chunk is at most 2 * nw inputs; the inputs are dealt evenly over
+// ceil(nin / (2 nw)) chunks.
 // Generated code touches nothing else: no memory but LDS reads, no scalar
 // registers, no M0.
 #pragma once

@@ -132,7 +132,7 @@ Split split_for(int rows) {
 
 size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector<uint32_t> &seg_off) {
     const Split sp = split_for(rows);
-    const int jc = 2 * sp.nw, nchunks = (nin + jc - 1) / jc;
+    const int jc = 2 * sp.nw, nchunks = (nin + jc - 1) / jc, ch_size = (nin + nchunks - 1) / nchunks;
     seg_off.assign((size_t)sp.npass * nchunks * sp.nw, kNoSegment);
     Emitter e{code, (size_t)kRegionWords};
     // the region's first 64 words stay s_endpgm: no segment starts at offset 0
@@ -145,7 +145,7 @@ size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector
                 // segments start on 64-byte instruction-cache lines
                 while (e.n & 15) e.word(0xbf810000u);
                 seg_off[((size_t)pass * nchunks + ch) * sp.nw + g] = (uint32_t)(e.n * 4);
-                const int j0 = ch * jc, jn = nin - j0 < jc ? nin - j0 : jc;
+                const int j0 = ch * ch_size, jn = nin - j0 < ch_size ? nin - j0 : ch_size;
                 emit_segment(e, M, nin, sp.rbase(pass, g, rows), cnt, j0, jn);
             }
     if (e.overflow) return 0;
