@@ -570,6 +570,47 @@ def test_auto_body_uses_straight_line_for_segments(oracle):
     assert sch._lib.ec_set_body(sch._ctx, 3) == _native.EC_ERR_INVALID_ARG
 
 
+def test_straight_line_plans_evicted_and_shared_across_threads(oracle):
+    """Straight-line plan lifecycle: 70 share sets (past the 64 cached plans,
+    so evicted plans unload their modules) rebuild whole segments on
+    generated code, then 8 threads rebuild concurrently on the same new
+    share sets, racing to make each plan's module once; every result
+    against the segment."""
+    k, n, ess, stripes = 4, 10, 256, 512  # 64 tiles per segment
+    sch = scheme(k, n, ess)
+    rng = np.random.default_rng(91)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    d_pieces = gpu_encode(sch, seg)
+    import itertools
+    sets = [list(c) for c in itertools.combinations(range(n), k) if any(x >= k for x in c)]
+    rng.shuffle(sets)
+    for nums in sets[:70]:
+        assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), nums
+        assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
+    errors = []
+    fresh = sets[70:74]
+
+    def work(t):
+        try:
+            for rep in range(6):
+                nums = fresh[(t + rep) % len(fresh)]
+                out = torch.empty(stripes * k * ess, dtype=torch.uint8, device="cuda")
+                st = torch.cuda.Stream()
+                with torch.cuda.stream(st):
+                    eestream.SegmentCodec(sch).rebuild_segments(
+                        nums, [d_pieces.data_ptr() + j * stripes * ess for j in nums], stripes, out, nseg=1,
+                        piece_seg_stride=n * stripes * ess, out_seg_stride=stripes * k * ess)
+                st.synchronize()
+                if not np.array_equal(out.cpu().numpy(), seg):
+                    errors.append((t, rep))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+
+
 @pytest.mark.parametrize("extra,bad,scatter", [(2, 1, 0), (4, 1, 0), (4, 2, 0), (6, 2, 40), (8, 3, 200), (4, 3, 0)])
 def test_decode_bad_pieces_over_long_runs(oracle, extra, bad, scatter):
     """Decode (Correct + Rebuild) of shares covering many stripes, with whole
