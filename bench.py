@@ -72,6 +72,7 @@ def parse():
                          "and optimised-variant samples)")
     ap.add_argument("--body", choices=["auto", "jump-table", "straight-line"], default="auto",
                     help="ec_set_body for the bench's context (include/uplink_ec.h); default: the library's choice")
+    ap.add_argument("--lib", default=None, help="another build of libuplink_ec.so (A/B runs of library variants)")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -283,7 +284,7 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    L = _native.load()
+    L = _native.load(args.lib) if args.lib else _native.load()
     if L.ec_set_device(torch.cuda.current_device()) != 0:
         raise RuntimeError("ec_set_device failed")
     ctx = ctypes.c_void_p()

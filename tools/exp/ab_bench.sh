@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B of two library builds in the bench (GPU box), alternating A B A B:
+#   bash tools/exp/ab_bench.sh OUTDIR LIB_A LIB_B [bench args]
+set -e
+O=$1; A=$2; B=$3; shift 3
+mkdir -p $O
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-other-configs --lib $A "$@" > $O/a$i.log 2>&1
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-other-configs --lib $B "$@" > $O/b$i.log 2>&1
+done
+echo done
