@@ -570,6 +570,35 @@ def test_auto_body_uses_straight_line_for_segments(oracle):
     assert sch._lib.ec_set_body(sch._ctx, 3) == _native.EC_ERR_INVALID_ARG
 
 
+LIBRARY_ENCODERS = {(29, 80), (20, 60), (4, 10), (2, 4), (20, 50), (30, 60), (50, 80)}  # rs_encoder_aot.def
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_codes_both_bodies(oracle, seed):
+    """Randomised: a random (k, n), share size and stripe count (some launches
+    above the 64-tile threshold, some below), a random share set with a random
+    number of extra shares, rebuilt through both bodies and the default, each
+    bit-exact against the oracle's encode of the same segment."""
+    rng = np.random.default_rng(seed * 7919 + 1)
+    k = int(rng.integers(1, 65))
+    n = int(rng.integers(k + 1, min(k + 70, 257)))
+    ess = int(rng.choice([16, 64, 256, 512, 4096]))
+    stripes = int(rng.integers(1, 2 + (1 << 22) // (k * ess)))
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    d_pieces = torch.from_numpy(np.ascontiguousarray(ref)).cuda().reshape(1, n, -1)
+    nums = sorted(rng.choice(n, k + int(rng.integers(0, n - k + 1)), replace=False).tolist())
+    # an encode that could start a run-time compilation (k <= 48, no library-built encoder) runs only
+    # on generated code here: a compilation nobody waits for would hold the process at exit
+    jit_able = ess % 16 == 0 and k <= 48 and n - k <= 96 and (k, n) not in LIBRARY_ENCODERS
+    for body in (_native.EC_BODY_JUMP_TABLE, _native.EC_BODY_STRAIGHT_LINE, _native.EC_BODY_AUTO):
+        assert sch._lib.ec_set_body(sch._ctx, body) == 0
+        if body == _native.EC_BODY_STRAIGHT_LINE or not jit_able:
+            assert np.array_equal(gpu_encode(sch, seg).cpu().numpy()[0], ref), (k, n, ess, stripes, body)
+        assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), (k, n, ess, stripes, body, nums)
+
+
 def test_straight_line_plans_evicted_and_shared_across_threads(oracle):
     """Straight-line plan lifecycle: 70 share sets (past the 64 cached plans,
     so evicted plans unload their modules) rebuild whole segments on

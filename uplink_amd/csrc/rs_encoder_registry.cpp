@@ -88,15 +88,18 @@ std::condition_variable g_cv;
 std::map<std::tuple<std::string, int, int>, std::unique_ptr<JitEntry>> g_jit;  // (arch, k, n)
 std::vector<std::thread> g_threads;  // compile threads (joined at exit)
 std::mutex g_compile_mu;             // one compilation at a time
+bool g_exiting = false;              // set at exit: queued compilations are skipped
 
 // Compile threads still running when the process exits must finish before the
 // HIP runtime tears itself down: the runtime registers its exit handler on its
 // first use, so this one, registered at the first compile (always later),
-// runs before it.
+// runs before it.  Only the compilation in progress is waited for; the ones
+// queued behind it give up (each takes seconds to a minute).
 void join_compiles() {
     std::vector<std::thread> t;
     {
         std::lock_guard<std::mutex> g(g_mu);
+        g_exiting = true;
         t.swap(g_threads);
     }
     for (auto &th : t)
@@ -111,6 +114,14 @@ std::string variant_expr(int k, int n, int nc, int nl) {
 // Compile (or read from the cache) the two variants of (k, n) for `arch`.
 void compile_entry(JitEntry *e, std::string arch, int k, int n) {
     std::lock_guard<std::mutex> serial(g_compile_mu);
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        if (g_exiting) {
+            e->state = JitEntry::kFailed;
+            g_cv.notify_all();
+            return;
+        }
+    }
     const std::string src = "#include \"rs_encoder.hpp\"\n";
     const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n), enc::full_loader_waves(k, n)),
                       parity = variant_expr(k, n, enc::parity_compute_waves(k, n), 4);
