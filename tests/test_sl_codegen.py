@@ -204,6 +204,17 @@ def test_random_matrices(rows, nin, zero_frac):
     check_matrix(M, rows + nin)
 
 
+def test_rows_without_terms():
+    """Rows with no nonzero coefficient, or whose first term comes in a later
+    chunk, or with a single term."""
+    rng = np.random.default_rng(3)
+    M = rng.integers(1, 256, (20, 29), dtype=np.uint8)
+    M[3] = 0
+    M[7, :16] = 0
+    M[12, 1:] = 0
+    check_matrix(M, 9)
+
+
 def test_oversize_plan_is_refused():
     """A plan whose code does not fit the 256-KiB region falls back to the
     jump table: generate() returns 0 words."""
