@@ -550,7 +550,7 @@ def test_straight_line_body_vs_oracle(oracle, k, n, ess, stripes):
     d_pieces = torch.from_numpy(np.ascontiguousarray(ref)).cuda().reshape(1, n, -1)
     for nums in (list(range(n - k, n)), sorted(rng.choice(n, k, replace=False).tolist())):
         assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), nums
-        if any(x >= k for x in nums) and k <= 64:  # RS(128,256)'s plans exceed the 256-KiB code region
+        if any(x >= k for x in nums):  # RS(128,256)'s plans take the 2-MiB code region
             assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
 
 

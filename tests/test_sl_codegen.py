@@ -44,10 +44,11 @@ def gf_mul_table():
     return GF_MUL
 
 
-def generate(M):
+def generate(M, cap=None):
     rows, nin = M.shape
     text = f"{rows} {nin}\n" + " ".join(str(int(x)) for x in M.reshape(-1)) + "\n"
-    out = subprocess.run([DUMP], input=text, capture_output=True, text=True, check=True).stdout.splitlines()
+    cmd = [DUMP] + ([str(cap)] if cap else [])
+    out = subprocess.run(cmd, input=text, capture_output=True, text=True, check=True).stdout.splitlines()
     nw, npass, nchunks = map(int, out[0].split()[1:])
     offs = [int(x) for x in out[1].split()[1:]]
     n = int(out[2].split()[1])
@@ -151,7 +152,7 @@ def check_matrix(M, seed):
     rows, nin = M.shape
     nw, npass, nchunks, offs, words = generate(M)
     assert len(offs) == npass * nchunks * nw
-    assert len(words) <= 65536
+    assert 0 < len(words) <= 524288  # the large region
     chs = -(-nin // nchunks)  # chunks dealt evenly (rs_kernels.hip)
     for pass_ in range(npass):
         p0 = pass_ * rows // npass
@@ -215,10 +216,14 @@ def test_rows_without_terms():
     check_matrix(M, 9)
 
 
-def test_oversize_plan_is_refused():
-    """A plan whose code does not fit the 256-KiB region falls back to the
-    jump table: generate() returns 0 words."""
+def test_region_sizes():
+    """A plan that does not fit the 256-KiB region is refused there
+    (generate() returns 0 words) and takes the 2-MiB one: the largest plan,
+    128 rows x 128 inputs of nonzero coefficients (two passes of eight
+    waves), fits it and computes the right products."""
     rng = np.random.default_rng(5)
     M = rng.integers(1, 256, (128, 128), dtype=np.uint8)
-    _, _, _, _, words = generate(M)
-    assert words == []
+    assert generate(M, cap=65536)[4] == []
+    words = generate(M)[4]
+    assert 65536 < len(words) <= 524288
+    check_matrix(M, 11)

@@ -9,7 +9,7 @@
    outputs compared with the segments; the time the first straight-line launch
    of a plan takes (code generation + module load + launch).
 3. The reference benchmark configurations' all-parity rebuilds.
-python tools/exp/sl_bench.py [--small-only | --k29-only]
+python tools/exp/sl_bench.py [--small-only | --k29-only | --big]
 """
 import ctypes
 import json
@@ -95,6 +95,10 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     run(L, 29, 80, 1, 64 * 29 * ESS - 4, s, small=True)
     if "--small-only" in sys.argv:
+        return
+    if "--big" in sys.argv:  # plans of the 2-MiB code region
+        for k, n in ((64, 96), (128, 256)):
+            run(L, k, n, 4, 64 << 20, s)
         return
     run(L, 29, 80, 16, 64 << 20, s)
     if "--k29-only" in sys.argv:

@@ -386,13 +386,13 @@ void ensure_sl(ec_ctx *c, MatPlan &plan) {
     if (plan.sl_tried) return;
     plan.sl_tried = true;
     if (plan.rows < 1 || plan.rows > kMaxOps || plan.nin < 1 || plan.nin > kMaxOps) return;
-    size_t roff = 0;
-    std::vector<uint8_t> img = sl::template_image(&roff);
-    std::vector<uint32_t> code(sl::kRegionWords);
-    memcpy(code.data(), img.data() + roff, code.size() * 4);
+    std::vector<uint32_t> code(sl::kRegionWords, 0xbf810000u);  // s_endpgm
     std::vector<uint32_t> offs;
-    if (!sl::generate(plan.M.data(), plan.rows, plan.nin, code.data(), offs)) return;  // does not fit
-    memcpy(img.data() + roff, code.data(), code.size() * 4);
+    const size_t used = sl::generate(plan.M.data(), plan.rows, plan.nin, code.data(), code.size(), offs);
+    if (!used) return;  // does not fit
+    size_t roff = 0, rwords = 0;
+    std::vector<uint8_t> img = sl::template_image(used, &roff, &rwords);
+    memcpy(img.data() + roff + 16, code.data() + 4, (used - 4) * 4);  // the marker words stay
     std::lock_guard<std::mutex> gs(c->setup_mu);
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;

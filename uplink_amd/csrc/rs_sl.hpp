@@ -35,12 +35,16 @@
 #define UPLINK_SL_MAGIC1 0x0b0d1e50
 #define UPLINK_SL_MAGIC2 0x2981e4c0
 #define UPLINK_SL_MAGIC3 0x7e91a7e5
-#define UPLINK_SL_REGION_WORDS 65536  // 256 KiB of code space per plan
+// code space per plan: two templates, 256 KiB and 2 MiB; a plan takes the
+// smaller one its code fits (rs_sl_region.hip is built once per size)
+#define UPLINK_SL_REGION_WORDS_SMALL 65536
+#define UPLINK_SL_REGION_WORDS_LARGE 524288
 
 namespace uplink_ec {
 namespace sl {
 
-constexpr int kRegionWords = UPLINK_SL_REGION_WORDS;
+constexpr int kRegionWordsSmall = UPLINK_SL_REGION_WORDS_SMALL;
+constexpr int kRegionWords = UPLINK_SL_REGION_WORDS_LARGE;  // the most any plan may use
 constexpr uint32_t kNoSegment = 0xffffffffu;
 
 // Row split of the runtime-matrix kernel (rs_kernels.hip) with a
@@ -53,16 +57,19 @@ struct Split {
 };
 Split split_for(int rows);  // the kernel launch (launch_matmul_sl) uses the same split
 
-// Generate the segments of M (rows x nin, row-major) into `code` (kRegionWords
-// words, pre-filled by the caller).  seg_off receives, for [pass][chunk]
-// [group], the byte offset of that segment in the region (kNoSegment when the
-// group has no rows in that pass).  Returns the number of words used, or 0
-// when the code does not fit the region.
-size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector<uint32_t> &seg_off);
+// Generate the segments of M (rows x nin, row-major) into `code` (cap words,
+// pre-filled by the caller).  seg_off receives, for [pass][chunk][group], the
+// byte offset of that segment in the region (kNoSegment when the group has no
+// rows in that pass).  Returns the number of words used, or 0 when the code
+// does not fit in cap words.  Any plan of up to 128 rows and 128 inputs fits
+// kRegionWords.
+size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, size_t cap, std::vector<uint32_t> &seg_off);
 
-// The template code object (an ELF) with its region restored (marker words +
-// s_endpgm fill); region_off receives the byte offset of the region in it.
-std::vector<uint8_t> template_image(size_t *region_off);
+// The template code object (an ELF) with room for `words` words of code
+// (the small template if they fit it, else the large one), its region
+// restored (marker words + s_endpgm fill); region_off receives the byte
+// offset of the region in it and region_words its size.
+std::vector<uint8_t> template_image(size_t words, size_t *region_off, size_t *region_words);
 
 }  // namespace sl
 }  // namespace uplink_ec

@@ -130,11 +130,11 @@ Split split_for(int rows) {
     return s;
 }
 
-size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector<uint32_t> &seg_off) {
+size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, size_t cap, std::vector<uint32_t> &seg_off) {
     const Split sp = split_for(rows);
     const int jc = 2 * sp.nw, nchunks = (nin + jc - 1) / jc, ch_size = (nin + nchunks - 1) / nchunks;
     seg_off.assign((size_t)sp.npass * nchunks * sp.nw, kNoSegment);
-    Emitter e{code, (size_t)kRegionWords};
+    Emitter e{code, cap};
     // the region's first 64 words stay s_endpgm: no segment starts at offset 0
     e.n = 64;
     for (int pass = 0; pass < sp.npass; pass++)
@@ -152,17 +152,23 @@ size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, std::vector
     return e.n;
 }
 
-std::vector<uint8_t> template_image(size_t *region_off) {
-    std::vector<uint8_t> img(sizeof(kSlHead) + (size_t)kRegionWords * 4 + sizeof(kSlTail));
-    memcpy(img.data(), kSlHead, sizeof(kSlHead));
-    uint32_t *r = (uint32_t *)(img.data() + sizeof(kSlHead));
+std::vector<uint8_t> template_image(size_t words, size_t *region_off, size_t *region_words) {
+    const bool small = words <= (size_t)kRegionWordsSmall;
+    const unsigned char *head = small ? kSlHead : kSlHeadLarge, *tail = small ? kSlTail : kSlTailLarge;
+    const size_t nhead = small ? sizeof(kSlHead) : sizeof(kSlHeadLarge);
+    const size_t ntail = small ? sizeof(kSlTail) : sizeof(kSlTailLarge);
+    const size_t nw = small ? (size_t)kRegionWordsSmall : (size_t)kRegionWords;
+    std::vector<uint8_t> img(nhead + nw * 4 + ntail);
+    memcpy(img.data(), head, nhead);
+    uint8_t *r = img.data() + nhead;
     const uint32_t magic[4] = {UPLINK_SL_MAGIC0, UPLINK_SL_MAGIC1, UPLINK_SL_MAGIC2, UPLINK_SL_MAGIC3};
-    for (int i = 0; i < kRegionWords; i++) {
+    for (size_t i = 0; i < nw; i++) {
         const uint32_t w = i < 4 ? magic[i] : 0xbf810000u;
-        memcpy((uint8_t *)r + 4 * (size_t)i, &w, 4);
+        memcpy(r + 4 * i, &w, 4);
     }
-    memcpy(img.data() + sizeof(kSlHead) + (size_t)kRegionWords * 4, kSlTail, sizeof(kSlTail));
-    *region_off = sizeof(kSlHead);
+    memcpy(img.data() + nhead + nw * 4, tail, ntail);
+    *region_off = nhead;
+    *region_words = nw;
     return img;
 }
 

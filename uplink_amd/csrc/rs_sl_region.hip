@@ -8,6 +8,7 @@
 // as a module (hipModuleLoadData).  The runtime-matrix kernel in the library
 // (rs_matmul_jt<NW, true>, rs_kernels.hip) then calls into that code.
 //
+// Built twice, with 256 KiB and 2 MiB regions (UPLINK_SL_REGION_WORDS).
 // The kernel jumps over the region, so none of its bytes run here.  The
 // region starts with four marker words (found and overwritten by the
 // library) and is filled with s_endpgm; the embedding script strips the fill
@@ -17,6 +18,9 @@
 
 #include "rs_sl.hpp"
 
+#ifndef UPLINK_SL_REGION_WORDS  // the Makefile builds one image per region size
+#define UPLINK_SL_REGION_WORDS UPLINK_SL_REGION_WORDS_SMALL
+#endif
 #define SL_STR2(x) #x
 #define SL_STR(x) SL_STR2(x)
 
