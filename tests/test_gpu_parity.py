@@ -640,8 +640,9 @@ def test_straight_line_plans_evicted_and_shared_across_threads(oracle):
     assert not errors, errors[:5]
 
 
+@pytest.mark.parametrize("body", BODIES)
 @pytest.mark.parametrize("extra,bad,scatter", [(2, 1, 0), (4, 1, 0), (4, 2, 0), (6, 2, 40), (8, 3, 200), (4, 3, 0)])
-def test_decode_bad_pieces_over_long_runs(oracle, extra, bad, scatter):
+def test_decode_bad_pieces_over_long_runs(oracle, extra, bad, scatter, body):
     """Decode (Correct + Rebuild) of shares covering many stripes, with whole
     shares corrupted (bad pieces: every column flagged) plus scattered errors
     in one other share.  ec_decode locates the bad shares on a sample of
@@ -650,6 +651,7 @@ def test_decode_bad_pieces_over_long_runs(oracle, extra, bad, scatter):
     codeword, the shares corrected in place, and TooManyErrors beyond e."""
     k, n, ln = 29, 80, 4096
     sch = scheme(k, n, 256)
+    assert sch._lib.ec_set_body(sch._ctx, body) == 0  # the re-encode and rebuild plans on either body
     rng = np.random.default_rng(extra * 100 + bad * 10 + scatter)
     data = rng.integers(0, 256, k * ln, dtype=np.uint8)
     allsh = oracle.FEC(k, n).encode(data)  # [n][ln]: byte column c of every share is one codeword
