@@ -599,6 +599,48 @@ def test_random_codes_both_bodies(oracle, seed):
         assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), (k, n, ess, stripes, body, nums)
 
 
+def test_per_stripe_calls_on_generated_code_many_threads(oracle):
+    """24 threads of per-stripe Rebuild and Decode with the straight-line body
+    forced: most calls make a new plan and module (random share sets, more
+    than the 64 cached plans, so plans are evicted and their modules unloaded
+    while other threads launch), every result against the stripe."""
+    k, n, ess = 20, 40, 256
+    sch = scheme(k, n, ess)
+    assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(23)
+    stripes = [rng.integers(0, 256, k * ess, dtype=np.uint8) for _ in range(4)]
+    allsh = [f.encode(st) for st in stripes]
+    errors = []
+
+    def work(t):
+        r = np.random.default_rng(500 + t)
+        try:
+            for rep in range(8):
+                i = (t + rep) % len(stripes)
+                if rep % 2 == 0:
+                    nums = sorted(r.choice(n, k, replace=False).tolist())
+                    got = np.zeros(k * ess, dtype=np.uint8)
+
+                    def put(sh, got=got):
+                        got[sh.number * ess:(sh.number + 1) * ess] = sh.data
+                    sch.rebuild([eestream.Share(j, np.array(allsh[i][j])) for j in nums], put)
+                else:
+                    nums = sorted(r.choice(n, k + 2, replace=False).tolist())
+                    sh = [eestream.Share(j, np.array(allsh[i][j])) for j in nums]
+                    sh[int(r.integers(0, len(sh)))].data[int(r.integers(0, ess))] ^= 0x77
+                    got = sch.decode(None, sh)
+                if not np.array_equal(np.asarray(got).reshape(-1), stripes[i]):
+                    errors.append((t, rep))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+    th = [threading.Thread(target=work, args=(t,)) for t in range(24)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errors, errors[:5]
+    assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
+
+
 def test_straight_line_plans_evicted_and_shared_across_threads(oracle):
     """Straight-line plan lifecycle: 70 share sets (past the 64 cached plans,
     so evicted plans unload their modules) rebuild whole segments on
