@@ -7,7 +7,7 @@ words are disassembled by the LLVM disassembler of the ROCm image (an
 encoder independent of the library's), and the disassembly is executed by a
 small emulator of the five instruction forms against GF(2^8) arithmetic from
 the oracle (oracle/infectious_np.py).  Every segment must:
-  * use only ds_read_b32 (from v126), s_waitcnt lgkmcnt, v_xor_b32,
+  * use only ds_read_b128 (from v126), s_waitcnt lgkmcnt, v_xor_b32,
     v_bitop3_b32 (0x96), and end in s_setpc_b64 s[48:49];
   * write only its rows' accumulators v[32 + 8o .. 39 + 8o] and the scratch
     v[96:125];
@@ -90,6 +90,10 @@ def vreg(s):
     return int(m.group(1))
 
 
+def busy(pending):
+    return {r for t in pending for r in t}
+
+
 def emulate(ins, lds, acc_rows):
     """Run one segment on one lane: `lds` maps byte offset -> 32-bit plane word,
     v[32 + 8o + p] start at 0.  Returns the accumulators and the registers
@@ -103,13 +107,15 @@ def emulate(ins, lds, acc_rows):
     ended = False
     for mn, ops in ins:
         assert not ended, "instruction after s_setpc_b64"
-        if mn == "ds_read_b32":
-            m = re.fullmatch(r"v(\d+), v126(?: offset:(\d+))?", ops)
+        if mn == "ds_read_b128":
+            m = re.fullmatch(r"v\[(\d+):(\d+)\], v126(?: offset:(\d+))?", ops)
             assert m, ops
-            d, off = int(m.group(1)), int(m.group(2) or 0)
-            v[d] = lds[off]
-            pending.append(d)
-            written.add(d)
+            d0, d1, off = int(m.group(1)), int(m.group(2)), int(m.group(3) or 0)
+            assert d1 == d0 + 3
+            for i in range(4):
+                v[d0 + i] = lds[off + 4 * i]
+                written.add(d0 + i)
+            pending.append(tuple(range(d0, d0 + 4)))
         elif mn == "s_waitcnt":
             m = re.fullmatch(r"lgkmcnt\((\d+)\)", ops)
             assert m, ops
@@ -117,14 +123,14 @@ def emulate(ins, lds, acc_rows):
             pending = pending[len(pending) - keep:] if keep else []
         elif mn in ("v_xor_b32_e32", "v_xor_b32"):
             d, a, b = (vreg(x) for x in ops.split(","))
-            assert a not in pending and b not in pending, "operand used before its LDS read landed"
+            assert not {a, b} & busy(pending), "operand used before its LDS read landed"
             v[d] = v[a] ^ v[b]
             written.add(d)
         elif mn == "v_bitop3_b32":
             m = re.fullmatch(r"(v\d+), (v\d+), (v\d+), (v\d+) bitop3:0x96", ops)
             assert m, ops
             d, a, b, c = (vreg(m.group(i)) for i in range(1, 5))
-            assert not {a, b, c} & set(pending)
+            assert not {a, b, c} & busy(pending)
             v[d] = v[a] ^ v[b] ^ v[c]
             written.add(d)
         elif mn == "s_setpc_b64":
@@ -161,9 +167,9 @@ def check_matrix(M, seed):
             j0, jn = ch * chs, min(chs, nin - ch * chs)
             x = rng.integers(0, 256, (jn, 32), dtype=np.uint8)
             lds = {}
-            for jj in range(jn):
+            for jj in range(jn):  # the straight-line layout (rs_device.hpp slice_inputs WIDE), lane 0
                 for p, w in enumerate(planes_of(x[jj])):
-                    lds[jj * 2048 + 256 * p] = w
+                    lds[jj * 2048 + 1024 * (p // 4) + 4 * (p % 4)] = w
             for g in range(nw):
                 rbase = p0 + g * prow // nw
                 cnt = p0 + (g + 1) * prow // nw - rbase

@@ -36,7 +36,10 @@ __device__ __forceinline__ void load_inputs(const RsArgs &a, int64_t seg, const 
     }
 }
 
-template <int NW, int PER, bool NT = false>
+// WIDE: the straight-line body's layout -- per input 2 KiB, planes 0-3 of a
+// lane as one 16-byte word at 16 lane, planes 4-7 at 1024 + 16 lane (two
+// ds_read_b128 per input, conflict-free); otherwise plane p at 256 p + 4 lane.
+template <int NW, int PER, bool NT = false, bool WIDE = false>
 __device__ __forceinline__ void slice_inputs(const RsArgs &a, int64_t seg, const TileCols &c, uint32_t *lds, int lane,
                                              int wave, int j0, int jn, bool do_copy, const StageRegs<PER> &r) {
     uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
@@ -52,9 +55,15 @@ __device__ __forceinline__ void slice_inputs(const RsArgs &a, int64_t seg, const
             }
             uint32_t w[8] = {r.A[i].x, r.A[i].y, r.A[i].z, r.A[i].w, r.B[i].x, r.B[i].y, r.B[i].z, r.B[i].w};
             bitslice8(w);
-            uint32_t *dst = lds + j * 8 * 64 + lane;
+            if constexpr (WIDE) {
+                u32x4 *dst = (u32x4 *)(lds + j * 8 * 64) + lane;
+                dst[0] = (u32x4){w[0], w[1], w[2], w[3]};
+                dst[64] = (u32x4){w[4], w[5], w[6], w[7]};
+            } else {
+                uint32_t *dst = lds + j * 8 * 64 + lane;
 #pragma unroll
-            for (int p = 0; p < 8; p++) dst[p * 64] = w[p];
+                for (int p = 0; p < 8; p++) dst[p * 64] = w[p];
+            }
         }
     }
 }

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
-    const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 4;
+    const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * (SL ? 16 : 4);
     // Plane chunks alternate between two LDS buffers, so one barrier per chunk
     // suffices: a wave staging chunk c+1 has passed barrier c, which every wave
     // reached only after it finished reading chunk c-1 from that buffer.
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             load_inputs<NW, PER, true>(a, seg, c, wave, 0, a.nin < CH ? a.nin : CH, r);
             for (int j0 = 0; j0 < a.nin; j0 += CH) {
                 const int jn = a.nin - j0 < CH ? a.nin - j0 : CH;
-                slice_inputs<NW, PER, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
+                slice_inputs<NW, PER, true, SL>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
                 lds_barrier();
                 // the next chunk's loads are in flight while this chunk is multiplied in
                 if (j0 + CH < a.nin) {

@@ -4,7 +4,7 @@
 // Five gfx950 instruction forms are emitted, encoded here directly (each
 // encoding is checked against the LLVM disassembler and a CPU emulation of
 // the generated code in tests/test_sl_codegen.py):
-//   ds_read_b32    vD, v126 offset:O     plane p of input jj: O = 2048 jj + 256 p
+//   ds_read_b128   v[D:D+3], v126 offset:O  planes 0-3 / 4-7 of input jj: O = 2048 jj (+ 1024)
 //   s_waitcnt      lgkmcnt(N)
 //   v_xor_b32_e32  vD, vA, vB            4-plane combinations; single-combination rows
 //   v_bitop3_b32   vD, vD, vL, vH 0x96   acc ^= lo[L] ^ hi[H]
@@ -20,11 +20,23 @@ namespace sl {
 
 namespace {
 
-constexpr int kAcc = 32, kLoBase = 95, kHiBase = 110, kXa = 126;
+constexpr int kAcc = 32, kXa = 126;
 constexpr int kRows = 8;  // accumulator rows per wave (rs_kernels.hip kJtRows)
 
-uint32_t lo_reg(int L) { return (uint32_t)(kLoBase + L); }
-uint32_t hi_reg(int H) { return (uint32_t)(kHiBase + H); }
+// The input's planes land by two ds_read_b128: planes 0-3 (lo[1], lo[2],
+// lo[4], lo[8]) in v[96:99], planes 4-7 (hi[...]) in v[100:103]; the other
+// combinations follow, lo in v[104:114], hi in v[115:125].
+constexpr int combo_slot(int m) {  // index of m among the 11 multi-bit nibbles
+    int i = 0;
+    for (int x = 1; x < m; x++) i += (x & (x - 1)) != 0;
+    return i;
+}
+uint32_t lo_reg(int L) {
+    return (uint32_t)((L & (L - 1)) == 0 ? 96 + (L == 1 ? 0 : L == 2 ? 1 : L == 4 ? 2 : 3) : 104 + combo_slot(L));
+}
+uint32_t hi_reg(int H) {
+    return (uint32_t)((H & (H - 1)) == 0 ? 100 + (H == 1 ? 0 : H == 2 ? 1 : H == 4 ? 2 : 3) : 115 + combo_slot(H));
+}
 
 struct Emitter {
     uint32_t *code;
@@ -35,8 +47,8 @@ struct Emitter {
         else overflow = true;
         n++;
     }
-    void ds_read_b32(uint32_t vdst, uint32_t vaddr, uint32_t offset) {
-        word(0xd86c0000u | (offset & 0xffffu));
+    void ds_read_b128(uint32_t vdst, uint32_t vaddr, uint32_t offset) {
+        word(0xd9fe0000u | (offset & 0xffffu));
         word((vdst << 24) | vaddr);
     }
     void waitcnt_lgkm(uint32_t cnt) { word(0xbf8cc07fu | ((cnt & 15u) << 8)); }
@@ -73,12 +85,13 @@ void emit_segment(Emitter &e, const uint8_t *M, int nin, int rbase, int cnt, int
             if (need_hi[m]) need_hi[m ^ low_bit(m)] = need_hi[low_bit(m)] = true;
         }
         need_lo[0] = need_hi[0] = false;
+        // input jj at 2048 jj: planes 0-3 of the lane at +16 lane, planes 4-7 at +1024 +16 lane
         const uint32_t base = (uint32_t)jj * 2048u;
-        int nhi = 0;
-        for (int q = 0; q < 4; q++)
-            if (need_lo[1 << q]) e.ds_read_b32(lo_reg(1 << q), kXa, base + 256u * q);
-        for (int q = 0; q < 4; q++)
-            if (need_hi[1 << q]) e.ds_read_b32(hi_reg(1 << q), kXa, base + 256u * (4 + q)), nhi++;
+        bool any_lo = false, any_hi = false;
+        for (int q = 0; q < 4; q++) any_lo |= need_lo[1 << q], any_hi |= need_hi[1 << q];
+        const int nhi = any_hi ? 1 : 0;
+        if (any_lo) e.ds_read_b128(96, kXa, base);
+        if (any_hi) e.ds_read_b128(100, kXa, base + 1024u);
         bool lo_combo = false, hi_combo = false;
         for (int m = 1; m < 16; m++) {
             if (m != low_bit(m)) lo_combo |= need_lo[m], hi_combo |= need_hi[m];
