@@ -16,13 +16,15 @@
 // runtime-matrix kernel calls segment (pass, chunk, group) through a table
 // of absolute addresses, once per chunk.
 //
-// Register contract (shared with rs_matmul_jt<NW, true> in rs_kernels.hip and
-// with the jump table's layout): accumulators v[32:95] (row o, plane p at
-// v[32 + 8o + p]); lo[L] = v[95 + L], hi[H] = v[110 + H] (L, H = 1..15) as
-// scratch; v126 = LDS byte address of plane 0 of the chunk's first input for
-// this lane (input jj at +2048 jj, plane p at +256 p); return address s[48:49].
-// A chunk is at most 2 * nw inputs; the inputs are dealt evenly over
-// ceil(nin / (2 nw)) chunks.
+// Register contract (shared with rs_matmul_jt<NW, true> in rs_kernels.hip;
+// the same registers as the jump table's): accumulators v[32:95] (row o,
+// plane p at v[32 + 8o + p]); v[96:125] scratch -- the input's planes 0-3 in
+// v[96:99] and 4-7 in v[100:103], then the 4-plane combinations; v126 = LDS
+// byte address of the chunk's first input for this lane, in the wide layout of
+// rs_device.hpp slice_inputs (input jj at +2048 jj, planes 0-3 of the lane as
+// one 16-byte word at +0, planes 4-7 at +1024; the lane's 16 bytes are folded
+// into v126); return address s[48:49].  A chunk is at most 2 * nw inputs; the
+// inputs are dealt evenly over ceil(nin / (2 nw)) chunks.
 // Generated code touches nothing else: no memory but LDS reads, no scalar
 // registers, no M0.
 #pragma once
