@@ -1,7 +1,7 @@
 // Template code object of the straight-line rebuild bodies (rs_sl_codegen.cpp).
 //
 // Built on its own (hipcc --genco) and embedded in the library
-// (tools/gen/embed_sl_image.py -> rs_sl_image.inc).  Its one kernel,
+// (tools/gen/embed_sl_image.py -> <build dir>/obj/rs_sl_image.inc).  Its one kernel,
 // rs_sl_where, writes the absolute address of `region`: a block of code
 // space inside its own text that the library fills, per decode matrix, with
 // generated straight-line multiply-accumulate code before it loads the image
