@@ -381,11 +381,17 @@ def main():
     by_set = {}
     for e, i in full:
         by_set.setdefault(i, []).append(e[1].elapsed_time(e[2]) * 1e3 / B)
+    # every rank's wall time (shard imbalance shows here) and a count of the ranks that took part
+    rank_walls, ranks_seen = [round(wall, 6)], 1
     if world > 1:
         import torch.distributed as dist
-        tw = torch.tensor([wall], dtype=torch.float64, device=coll_dev or dev)
-        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
-        wall = float(tw.item())
+        walls = [torch.zeros(1, dtype=torch.float64, device=coll_dev or dev) for _ in range(world)]
+        dist.all_gather(walls, torch.tensor([wall], dtype=torch.float64, device=coll_dev or dev))
+        rank_walls = [round(float(w.item()), 6) for w in walls]
+        seen = torch.ones(1, dtype=torch.int64, device=coll_dev or dev)
+        dist.all_reduce(seen, op=dist.ReduceOp.SUM)
+        ranks_seen = int(seen.item())
+        wall = max(rank_walls)
 
     # correctness (outside the timed region): a full launch pair per pool slot rebuilds its input, and
     # one segment's pieces match the oracle
@@ -479,14 +485,22 @@ def main():
     del cpy_a, cpy_b
     dominant = "encode" if t_enc_full >= t_dec_full else "decode"
     dk = kernels[dominant]
-    traffic = None
+    # PMC traffic of the dominant kernel, from the record tools/prof_round.sh wrote for one build:
+    # used only when that build is the library running here (ec_build_id) and the batch matches
+    traffic, traffic_note = None, None
     try:
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        if tj.get("segments_per_launch", 8) == B:  # PMC bytes are per launch of this batch size
+        build = L.ec_build_id().decode()
+        if tj.get("build_id") != build:
+            traffic_note = f"{args.traffic_json} was taken from build {tj.get('build_id')}, this is {build}"
+        elif tj.get("segments_per_launch") != B:
+            traffic_note = f"{args.traffic_json} is per launch of {tj.get('segments_per_launch')} segments, not {B}"
+        else:
             traffic = tj.get(dominant, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+            traffic_note = f"rocprofv3 FETCH_SIZE/WRITE_SIZE of build {build}: {tj.get(dominant, {}).get('kernels')}"
+    except (OSError, ValueError) as e:
+        traffic_note = f"no PMC record: {e}"
     line = {
         "metric": "GiB/s erasure encode+decode (device-resident), RS(29,80) 64 MiB segments",
         "value": round(value, 2),
@@ -508,7 +522,7 @@ def main():
                    "parallelism": f"segments sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(dk["achieved_GBps"], 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic, "frac_parity_only_encode": par_frac,
+                     "traffic": traffic, "traffic_note": traffic_note, "frac_parity_only_encode": par_frac,
                      "frac_decode": round(dec_gbps / HBM_PEAK_GBPS, 4),
                      "copy_GBps_on_box": round(copy_gbps, 1),
                      "frac_of_copy": round(dk["achieved_GBps"] / copy_gbps, 4)},
@@ -517,6 +531,9 @@ def main():
         "decode_gibps": round(B * S_PAD / 2**30 / t_dec_full, 2),
         "gpu_busy_s": round(t_enc + t_dec, 4),
         "segments_timed_this_rank": seg_launched,
+        "ranks_seen": ranks_seen,
+        "rank_wall_s": rank_walls,
+        "build_id": L.ec_build_id().decode(),
         "verified": verified,
     }
     if rank == 0 and world == 1 and not args.no_other_configs:

@@ -245,6 +245,11 @@ int ec_set_body(ec_ctx *ctx, int body);
 /* which body the ctx's last runtime-matrix launch used: EC_BODY_JUMP_TABLE,
  * EC_BODY_STRAIGHT_LINE, or EC_BODY_AUTO when there was none yet */
 int ec_last_body(const ec_ctx *ctx);
+/* Identity of this build: 16 hex digits of a SHA-256 over the library's
+ * sources, generators and build flags (uplink_amd/csrc/Makefile).  Measurement
+ * records taken from one build (profiles/pmc_traffic.json) carry it, so a bench
+ * run of another build can tell they are stale.  No reference counterpart. */
+const char *ec_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -111,6 +111,33 @@ def test_put_get_roundtrip_cpu(cpu_rs):
     assert nodes[9] is None and nodes[5] is None
 
 
+class _BrokenOnCancelStore(ecclient.LoopbackPieceStore):
+    """Slow nodes that fail with a plain I/O error (not context.Canceled) once
+    the long-tail cut has canceled them, as a transport torn down under them
+    does."""
+
+    def put_piece(self, limit, reader, cancel):
+        if limit.node_id in self.delay:
+            cancel.wait(self.delay[limit.node_id])
+            if cancel.is_set():
+                raise IOError("connection reset by peer")
+        return super().put_piece(limit, reader, cancel)
+
+
+def test_put_error_after_cut_counts_as_canceled(cpu_rs):
+    """client.go:232-243: once the pieces context is canceled, PutPiece
+    reports the upload as cut due to a slow connection (context.Canceled the
+    primary error) whatever the store returned; a failure before the cut stays
+    an "upload failed"."""
+    rng = np.random.default_rng(11)
+    lim = limits_for(10, 11)
+    store = _BrokenOnCancelStore(delay={lim[2].node_id: 5.0, lim[6].node_id: 5.0})
+    c = ecclient.ECClient(store)
+    nodes, _ = c.put(lim, cpu_rs, io.BytesIO(rng.bytes(50_000)))
+    assert c.last_counts == {"total": 10, "optimal": 8, "successful": 8, "failed": 0, "canceled": 2}
+    assert nodes[2] is None and nodes[6] is None
+
+
 def test_put_single_result_cpu(cpu_rs):
     c = ecclient.ECClient(ecclient.LoopbackPieceStore())
     res = c.put_single_result(limits_for(10, 3), cpu_rs, io.BytesIO(b"hello" * 999))

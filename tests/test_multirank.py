@@ -96,3 +96,7 @@ def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
     assert line["n_gpus"] == 2 and line["verified"] is True
     assert line["config"]["total_segments_per_step"] == 64 and line["config"]["segments_this_rank"] == 32
     assert line["value"] > 0
+    # the record shows that both ranks took part, and each rank's own wall time
+    assert line["ranks_seen"] == 2
+    assert len(line["rank_wall_s"]) == 2 and all(w > 0 for w in line["rank_wall_s"])
+    assert line["ms_per_step"] == pytest.approx(max(line["rank_wall_s"]) / line["steps"] * 1e3, rel=1e-3)

@@ -43,7 +43,11 @@ def family(match):
             "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": int(rd + wr)}
 
 
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from uplink_amd import _native  # noqa: E402  (the build the passes ran: bench.py loads the same library)
+
 res = {
+    "build_id": _native.load().ec_build_id().decode(),
     "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, --kernel-trace) of `python3 bench.py "
               f"--steps 3 --warmup 1 --settle-s 0 --no-cpu-baseline --no-other-configs` ({B} RS(29,80) 64 MiB segments per launch); mean "
               "over dispatches; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py",

@@ -88,6 +88,7 @@ SIGNATURES = {
     "ec_prepare_encoder": (ctypes.c_int, [vp, ctypes.c_int]),
     "ec_set_body": (ctypes.c_int, [vp, ctypes.c_int]),
     "ec_last_body": (ctypes.c_int, [vp]),
+    "ec_build_id": (ctypes.c_char_p, []),
 }
 
 _lib = None

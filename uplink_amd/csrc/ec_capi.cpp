@@ -50,10 +50,37 @@ struct MatPlan {
     bool sl_tried = false;
     hipModule_t sl_mod = nullptr;
     uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
+    // Completion of the plan's launches: one event per caller stream, recorded
+    // behind the stream's latest launch of this plan (note_use).  Teardown
+    // waits on these alone -- a launch that used the plan may still be in
+    // flight when its last reference goes -- instead of synchronising the
+    // whole device (other contexts' and unrelated work included).
+    std::mutex use_mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    static constexpr size_t kMaxUseStreams = 16;
+    void note_use(hipStream_t s) {
+        std::lock_guard<std::mutex> g(use_mu);
+        for (auto &u : uses)
+            if (u.first == s) {
+                (void)hipEventRecord(u.second, s);
+                return;
+            }
+        hipEvent_t e = nullptr;
+        if (uses.size() >= kMaxUseStreams) {
+            // the oldest stream's entry: once its last launch of this plan is
+            // done it has nothing in flight here, and its event can be reused
+            e = uses.front().second;
+            (void)hipEventSynchronize(e);
+            uses.erase(uses.begin());
+        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamSynchronize(s);  // no event: make this launch finish now instead
+            return;
+        }
+        (void)hipEventRecord(e, s);
+        uses.emplace_back(s, e);
+    }
     ~MatPlan() {
-        // a launch that used this plan may still be in flight (its last
-        // reference can go while a caller's stream runs it)
-        if (sl_mod) (void)hipDeviceSynchronize();
+        for (auto &u : uses) (void)hipEventSynchronize(u.second), (void)hipEventDestroy(u.second);
         if (d_coef) (void)hipFree(d_coef);
         for (uint64_t *t : d_tgt)
             if (t) (void)hipFree(t);
@@ -199,7 +226,26 @@ Workspace *acquire_ws(ec_ctx *c, size_t need, size_t host_need = 0) {
     return w;
 }
 
+// Staging above this size is given back after use rather than kept for the
+// life of the context (a burst of large per-stripe calls would otherwise pin it).
+constexpr size_t kWsKeepBytes = (size_t)32 << 20;
+
+void shrink_ws(Workspace *w) {
+    if (w->cap > kWsKeepBytes && w->d_buf) {
+        if (w->stream) (void)hipStreamSynchronize(w->stream);
+        (void)hipFree(w->d_buf);
+        w->d_buf = nullptr;
+        w->cap = 0;
+    }
+    if (w->h_cap > kWsKeepBytes && w->h_buf) {
+        (void)hipHostFree(w->h_buf);
+        w->h_buf = nullptr;
+        w->h_cap = 0;
+    }
+}
+
 void release_ws(ec_ctx *c, Workspace *w) {
+    shrink_ws(w);
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->ws_waiters.empty()) {
         WsWaiter *next = c->ws_waiters.front();
@@ -301,8 +347,10 @@ int cached_plan(ec_ctx *c, const std::vector<int> &key, F &&make_matrix, PlanPtr
             c->plans.pop_back();
         }
     }
-    // an evicted plan may still be read by launches in flight on callers' streams
-    if (!evicted.empty()) (void)hipDeviceSynchronize();
+    // an evicted plan may still be read by launches in flight on callers'
+    // streams: its destructor (here, or wherever its last reference goes)
+    // waits for exactly those launches (MatPlan::note_use)
+    evicted.clear();
     *out = p;
     return EC_OK;
 }
@@ -455,6 +503,7 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64
             HIP_TRY(launch_matmul_bytes(a, s));
             a.total_tiles = keep;
         }
+        plan.note_use(s);
         if (int rc = after_launch(c->d_chk, s)) return rc;
         done += rows;
         blk++;
@@ -549,6 +598,15 @@ int ec_set_body(ec_ctx *c, int body) {
 }
 
 int ec_last_body(const ec_ctx *c) { return c ? c->last_body : EC_BODY_AUTO; }
+
+// UPLINK_EC_BUILD_ID: generated by the Makefile into the build directory
+// (build_id.inc) from a digest of the sources, generators and flags.
+const char *ec_build_id(void) {
+    static const char id[] =
+#include "build_id.inc"
+        ;
+    return id;
+}
 
 int ec_device_count(void) {
     int n = 0;
@@ -798,7 +856,13 @@ static int run_single_batch(ec_ctx *c, SingleReq *const *req, size_t nreq, size_
     Workspace *w = acquire_ws(c, out_at + out_bytes + 64, h_out + out_bytes);
     if (!w->d_buf || !w->stream || !w->h_buf) {
         release_ws(c, w);
-        return EC_ERR_DEVICE;
+        if (nreq == 1) return EC_ERR_DEVICE;
+        // no room for the whole batch: each half on its own (a request that
+        // would succeed alone does not fail for sharing a batch)
+        const size_t h = nreq / 2;
+        const int r1 = run_single_batch(c, req, h, bs), r2 = run_single_batch(c, req + h, nreq - h, bs);
+        for (size_t r = 0; r < h; r++) req[r]->rc = r1;
+        return r2;
     }
     for (size_t r = 0; r < nreq; r++) {
         memcpy(w->h_buf + r * stripe, req[r]->in, stripe);
@@ -856,7 +920,11 @@ static int run_single_batch(ec_ctx *c, SingleReq *const *req, size_t nreq, size_
     return rc;
 }
 
+// A batch takes queued requests up to this many, and up to kMaxSingleBatchBytes
+// of stripes (at least one request): the staging it needs stays bounded however
+// large the callers' stripes are.
 constexpr size_t kMaxSingleBatch = 2048;
+constexpr size_t kMaxSingleBatchBytes = (size_t)16 << 20;
 constexpr int kSingleLeaders = 2;  // batches in flight at once: one's host copies overlap the other's GPU work
 
 // EncodeSingle (rs.go:21-23), called by uplink per (piece, stripe) from up to
@@ -890,7 +958,10 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
             continue;
         }
         c->single_leaders++;
-        const size_t take = std::min(c->single_q.size(), kMaxSingleBatch);
+        size_t take = 0, bytes = 0;
+        while (take < c->single_q.size() && take < kMaxSingleBatch &&
+               (take == 0 || bytes + c->single_q[take]->bs * c->k <= kMaxSingleBatchBytes))
+            bytes += c->single_q[take++]->bs * c->k;
         std::vector<SingleReq *> batch(c->single_q.begin(), c->single_q.begin() + take);
         c->single_q.erase(c->single_q.begin(), c->single_q.begin() + take);
         for (SingleReq *q : batch) q->taken = true;
@@ -900,8 +971,10 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
         for (size_t i = 0; i < batch.size();) {
             size_t j = i;
             while (j < batch.size() && batch[j]->bs == batch[i]->bs) j++;
+            for (size_t q = i; q < j; q++) batch[q]->rc = EC_OK;
             const int rc = run_single_batch(c, batch.data() + i, j - i, batch[i]->bs);
-            for (size_t q = i; q < j; q++) batch[q]->rc = rc;
+            for (size_t q = i; q < j; q++)
+                if (batch[q]->rc == EC_OK) batch[q]->rc = rc;
             i = j;
         }
         lk.lock();

@@ -169,9 +169,12 @@ class ECClient:
                 return None
             try:
                 return self.store.put_piece(limit, reader, cancel)
-            except Canceled as e:
-                raise ECClientError(f"upload cut due to slow connection (node:{limit.node_id.hex()}): {e}", e)
             except Exception as e:  # noqa: BLE001 - the reference wraps every upload error
+                if cancel.is_set():
+                    # client.go:232-243: once the pieces context is canceled, whatever the store
+                    # returned is a cancel, with context.Canceled the primary error of the chain
+                    raise ECClientError(f"upload cut due to slow connection (node:{limit.node_id.hex()}): {e}",
+                                        e if isinstance(e, Canceled) else Canceled(f"context canceled: {e}"))
                 raise ECClientError(f"upload failed (node:{limit.node_id.hex()}, address:{limit.address}): {e}", e)
         finally:
             if hasattr(reader, "close"):
