@@ -38,20 +38,31 @@ __device__ __forceinline__ v4 ldnt(const uint8_t *p) { return __builtin_nontempo
 __device__ __forceinline__ void stnt(uint8_t *p, v4 v) { __builtin_nontemporal_store(v, (v4 *)p); }
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+struct Opt {
+    int64_t pstride;  // bytes between piece streams (PLEN in the real layout)
+    int contig;       // 1: a tile's 80 rows written contiguously ([tile][80][CPL KiB])
+    int copy;         // write the 29 data pieces
+    int read;         // load the inputs (0: rows made from registers)
+    int order;        // 1: consecutive blocks take consecutive segments (seg = b % NSEG)
+};
+
 template <int NW, int CPL>
 __device__ __forceinline__ void do_tile(const uint8_t *in, uint8_t *out, int64_t tile, v4 *lds, int fake, int lane,
-                                        int wave) {
+                                        int wave, const Opt o) {
     constexpr int64_t TPS = CPS / (64 * CPL);
     constexpr int PER = (K + NW - 1) / NW, PR = (R + NW - 1) / NW;
-    const int64_t seg = tile / TPS, tt = tile - seg * TPS;
+    int64_t seg = tile / TPS, tt = tile - seg * TPS;
+    if (o.order) seg = tile % NSEG, tt = tile / NSEG;
     const uint8_t *is = in + seg * SPAD;
-    uint8_t *os = out + seg * (int64_t)N * PLEN;
+    uint8_t *os = out + seg * (int64_t)N * o.pstride;
     int64_t qin[CPL], qout[CPL];
+    const int64_t pst = o.contig ? (int64_t)CPL * 1024 : o.pstride;
+    if (o.contig) os = out + (seg * TPS + tt) * (int64_t)N * CPL * 1024;
 #pragma unroll
     for (int c = 0; c < CPL; c++) {
         const int64_t q = tt * 64 * CPL + c * 64 + lane;
         qin[c] = (q >> 4) * (K * ESS) + (q & 15) * 16;
-        qout[c] = q * 16;
+        qout[c] = o.contig ? (c * 64 + lane) * 16 : q * 16;
     }
     v4 x[PER][CPL];
 #pragma unroll
@@ -59,7 +70,8 @@ __device__ __forceinline__ void do_tile(const uint8_t *in, uint8_t *out, int64_t
         const int j = wave + NW * i;
         if (j < K)
 #pragma unroll
-            for (int c = 0; c < CPL; c++) x[i][c] = ldnt(is + j * ESS + qin[c]);
+            for (int c = 0; c < CPL; c++)
+                x[i][c] = o.read ? ldnt(is + j * ESS + qin[c]) : (v4){(uint32_t)j, (uint32_t)c, (uint32_t)lane, 7u};
     }
 #pragma unroll
     for (int i = 0; i < PER; i++) {
@@ -67,7 +79,7 @@ __device__ __forceinline__ void do_tile(const uint8_t *in, uint8_t *out, int64_t
         if (j < K)
 #pragma unroll
             for (int c = 0; c < CPL; c++) {
-                stnt(os + j * PLEN + qout[c], x[i][c]);
+                if (o.copy) stnt(os + j * pst + qout[c], x[i][c]);
                 lds[(j * CPL + c) * 64 + lane] = x[i][c];
             }
     }
@@ -94,24 +106,25 @@ __device__ __forceinline__ void do_tile(const uint8_t *in, uint8_t *out, int64_t
             for (int c = 0; c < CPL; c++) {
                 v4 v = lds[((r % K) * CPL + c) * 64 + lane] ^ lds[(((r + 7) % K) * CPL + c) * 64 + lane];
                 v.x ^= salt;
-                stnt(os + (K + r) * PLEN + qout[c], v);
+                stnt(os + (K + r) * pst + qout[c], v);
             }
     }
 }
 
 template <int NW, int CPL>
-__global__ __launch_bounds__(NW * 64) void oneshot(const uint8_t *in, uint8_t *out, int fake) {
+__global__ __launch_bounds__(NW * 64) void oneshot(const uint8_t *in, uint8_t *out, int fake, const Opt o) {
     extern __shared__ v4 lds[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    do_tile<NW, CPL>(in, out, blockIdx.x, lds, fake, lane, wave);
+    do_tile<NW, CPL>(in, out, blockIdx.x, lds, fake, lane, wave, o);
 }
 
 template <int NW, int CPL>
-__global__ __launch_bounds__(NW * 64) void persist(const uint8_t *in, uint8_t *out, int fake, int64_t ntiles) {
+__global__ __launch_bounds__(NW * 64) void persist(const uint8_t *in, uint8_t *out, int fake, int64_t ntiles,
+                                                   const Opt o) {
     extern __shared__ v4 lds[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        do_tile<NW, CPL>(in, out, t, lds, fake, lane, wave);
+        do_tile<NW, CPL>(in, out, t, lds, fake, lane, wave, o);
         lds_barrier();
     }
 }
@@ -119,9 +132,11 @@ __global__ __launch_bounds__(NW * 64) void persist(const uint8_t *in, uint8_t *o
 int main(int argc, char **argv) {
     uint8_t *in, *out;
     CK(hipMalloc(&in, SPAD * NSEG));
-    CK(hipMalloc(&out, (int64_t)N * PLEN * NSEG));
+    const int64_t OUTB = (int64_t)N * (PLEN + (1 << 20)) * NSEG;  // room for padded piece strides
+    CK(hipMalloc(&out, OUTB));
     CK(hipMemset(in, 0x5a, SPAD * NSEG));
-    CK(hipMemset(out, 0x33, (int64_t)N * PLEN * NSEG));
+    CK(hipMemset(out, 0x33, OUTB));
+    Opt o = {PLEN, 0, 1, 1, 0};
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     hipEvent_t e0, e1;
@@ -152,7 +167,7 @@ int main(int argc, char **argv) {
         const size_t lb = (size_t)K * (CPL) * 1024 + (size_t)(PADKB) * 1024;                                     \
         char nm[128];                                                                                             \
         snprintf(nm, sizeof nm, "oneshot NW=%d CPL=%d fake=%d lds=%zuK", NW, CPL, fake, lb / 1024);              \
-        timeit(nm, [&] { hipLaunchKernelGGL((oneshot<NW, CPL>), dim3(nt), dim3(NW * 64), lb, 0, in, out, fake); }); \
+        timeit(nm, [&] { hipLaunchKernelGGL((oneshot<NW, CPL>), dim3(nt), dim3(NW * 64), lb, 0, in, out, fake, o); }); \
     }
 #define PERSIST(NW, CPL, SCALE, WPC, PADKB)                                                                         \
     {                                                                                                             \
@@ -162,7 +177,7 @@ int main(int argc, char **argv) {
         char nm[128];                                                                                             \
         snprintf(nm, sizeof nm, "persist NW=%d CPL=%d fake=%d wg/cu=%d lds=%zuK", NW, CPL, fake, WPC, lb / 1024); \
         timeit(nm, [&] {                                                                                          \
-            hipLaunchKernelGGL((persist<NW, CPL>), dim3(cus * (WPC)), dim3(NW * 64), lb, 0, in, out, fake, nt);   \
+            hipLaunchKernelGGL((persist<NW, CPL>), dim3(cus * (WPC)), dim3(NW * 64), lb, 0, in, out, fake, nt, o);\
         });                                                                                                       \
     }
     const int which = argc > 1 ? atoi(argv[1]) : 0;
@@ -181,6 +196,23 @@ int main(int argc, char **argv) {
         ONESHOT(16, 1, 1.0, 24) ONESHOT(8, 1, 1.0, 24)  // 53 KiB: 3 WGs per CU
         ONESHOT(16, 2, 0.6, 22) ONESHOT(16, 1, 0.6, 24)
         PERSIST(16, 2, 1.0, 2, 22) PERSIST(16, 1, 1.0, 3, 24)
+    }
+    if (which == 3) {
+        // what the memory system penalises, on the 1-KiB tile of 8 waves (CPL=1) and CPL=2
+        auto show = [&](const char *what) { printf("-- %s\n", what); };
+        show("real layout");
+        ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0)
+        o.contig = 1; show("a tile's 80 rows contiguous"); ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0) o.contig = 0;
+        o.copy = 0; show("no copy-through (parity only; TB/s over the full bytes)"); ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0) o.copy = 1;
+        o.read = 0; show("no reads (TB/s over the full bytes)"); ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0)
+        o.contig = 1; show("no reads, contiguous rows"); ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0) o.contig = 0; o.read = 1;
+        o.order = 1; show("blocks dealt over segments"); ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0) o.order = 0;
+        for (int64_t pad : {1024, 4096, 16384, 65536, 256 * 1024}) {
+            o.pstride = PLEN + pad;
+            printf("-- piece stride PLEN + %lld\n", (long long)pad);
+            ONESHOT(8, 1, 0, 0) ONESHOT(8, 2, 0, 0)
+        }
+        o.pstride = PLEN;
     }
     return 0;
 }

@@ -140,8 +140,23 @@ struct HostPipe {
     size_t in_cap = 0, out_cap = 0;
 };
 
+// Work counters of the compile-time encoder's launches (RsArgs::queue): a
+// ring of counters, each zeroed on the launch's stream right before it and
+// handed to no other launch until an event behind its last launch has
+// completed, so launches on different streams never share one.
+struct QueueRing {
+    static constexpr int kSlots = 32;
+    static constexpr int kStride = 64;  // words: one counter per 256 bytes
+    std::mutex mu;
+    uint32_t *d = nullptr;
+    hipEvent_t ev[kSlots] = {};
+    bool used[kSlots] = {}, busy[kSlots] = {};
+    int next = 0;
+};
+
 struct ec_ctx {
     int k = 0, n = 0, ess = 0, device = 0;
+    QueueRing qring;
     std::mutex pipe_mu;  // one host pipeline at a time per context
     HostPipe pipe;
     std::vector<uint8_t> G;        // n x k
@@ -264,6 +279,8 @@ void fill_geometry(RsArgs &a, int ess, int64_t nstripes, int64_t nseg) {
     a.chunks_per_seg = nstripes * (ess / 16);
     a.tiles_per_seg = (a.chunks_per_seg + 127) / 128;
     a.total_tiles = a.tiles_per_seg * nseg;
+    a.blocks_per_seg = (a.chunks_per_seg + 63) / 64;
+    a.total_blocks = a.blocks_per_seg * nseg;
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
@@ -406,6 +423,43 @@ int after_launch(uint32_t *chk, hipStream_t s) {
     (void)chk, (void)s;
 #endif
     return EC_OK;
+}
+
+// A zeroed work counter for one encoder launch on stream s (slot in *slot;
+// queue_done after the launch).  nullptr when none can be had: the kernel then
+// assigns its tiles statically, with identical results.
+uint32_t *queue_take(ec_ctx *c, hipStream_t s, int *slot) {
+    QueueRing &q = c->qring;
+    std::lock_guard<std::mutex> g(q.mu);
+    if (!q.d) {
+        if (hipMalloc(&q.d, sizeof(uint32_t) * QueueRing::kStride * QueueRing::kSlots) != hipSuccess) {
+            q.d = nullptr;
+            return nullptr;
+        }
+        for (int i = 0; i < QueueRing::kSlots; i++)
+            if (hipEventCreateWithFlags(&q.ev[i], hipEventDisableTiming) != hipSuccess) q.ev[i] = nullptr;
+    }
+    for (int tries = 0; tries < QueueRing::kSlots; tries++) {
+        const int i = q.next;
+        q.next = (q.next + 1) % QueueRing::kSlots;
+        if (q.busy[i] || !q.ev[i]) continue;
+        // the slot's previous launch (any stream) is done before this one zeroes it
+        if (q.used[i] && hipStreamWaitEvent(s, q.ev[i], 0) != hipSuccess) continue;
+        uint32_t *ctr = q.d + (size_t)i * QueueRing::kStride;
+        if (hipMemsetAsync(ctr, 0, sizeof(uint32_t), s) != hipSuccess) continue;
+        q.busy[i] = true;
+        *slot = i;
+        return ctr;
+    }
+    return nullptr;
+}
+
+void queue_done(ec_ctx *c, hipStream_t s, int slot) {
+    QueueRing &q = c->qring;
+    std::lock_guard<std::mutex> g(q.mu);
+    q.used[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
+    if (!q.used[slot]) (void)hipStreamSynchronize(s);  // no event: let the launch finish before the slot returns
+    q.busy[slot] = false;
 }
 
 // Launches of at least this many tiles use a plan's straight-line code under
@@ -669,6 +723,9 @@ void ec_destroy(ec_ctx *c) {
     c->enc_row.clear();
     if (c->setup) (void)hipStreamSynchronize(c->setup), (void)hipStreamDestroy(c->setup);
     if (c->d_chk) (void)hipFree(c->d_chk);
+    for (int i = 0; i < QueueRing::kSlots; i++)
+        if (c->qring.ev[i]) (void)hipEventSynchronize(c->qring.ev[i]), (void)hipEventDestroy(c->qring.ev[i]);
+    if (c->qring.d) (void)hipFree(c->qring.d);
     delete c;
 }
 
@@ -772,7 +829,11 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
         if (ek) {
             a.coef = nullptr;
             set_extents(a, (int64_t)nseg, c->d_chk);
-            HIP_TRY(launch_encode_special(*ek, a, 0, s));
+            int slot = -1;
+            a.queue = queue_take(c, s, &slot);
+            const hipError_t e = launch_encode_special(*ek, a, 0, s);
+            if (slot >= 0) queue_done(c, s, slot);
+            HIP_TRY(e);
             return after_launch(c->d_chk, s);
         }
     }

@@ -39,6 +39,11 @@ struct RsArgs {
     int64_t chunks_per_seg;   // nstripes * ess / 16
     int64_t tiles_per_seg;    // ceil(chunks_per_seg / 128)
     int64_t total_tiles;      // tiles_per_seg * nseg
+    // compile-time encoder: 1-KiB column blocks (64 chunks of one share row),
+    // paired across the batch (rs_tile.hpp pair_cols), handed out by a queue
+    int64_t blocks_per_seg;   // ceil(chunks_per_seg / 64)
+    int64_t total_blocks;     // blocks_per_seg * nseg
+    uint32_t *queue;          // zeroed work counter of this launch (null: static assignment)
     int32_t ess;              // erasure share size, multiple of 16 for the bit-sliced path
     int32_t cps;              // ess / 16 (16-byte chunks per share per stripe)
     int32_t nin;              // number of inputs (k)

@@ -83,6 +83,14 @@ __device__ __forceinline__ void compute_chunk(const uint32_t *lds, int lane, uin
     });
 }
 
+// Tile t for the n-th fetch of this workgroup: from the launch's work queue
+// (a.queue, zeroed before the launch) or, without one, statically.  Only one
+// lane calls it; a returning vector atomic, not a scalar one.
+__device__ __forceinline__ int32_t take_tile(const RsArgs &a, int n) {
+    if (a.queue) return (int32_t)atomicAdd(a.queue, 1u);
+    return (int32_t)(blockIdx.x + (int64_t)n * gridDim.x);
+}
+
 template <int K, int N, int NC, int NL>
 __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
     constexpr int R = N - K;
@@ -90,32 +98,47 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
     constexpr int NCH = chunks_of(K), KC = chunk_size(K);
     constexpr int PER = (KC + NL - 1) / NL;
     __shared__ uint32_t lds[2][KC * 8 * 64];
+    __shared__ int32_t s_q[4];  // tiles taken from the queue, in order (ring)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool loader = wave >= NC;
     const int lw = wave - NC;
-    // the workgroup's items: tiles blockIdx.x, +gridDim.x, ..., each as chunks 0 .. NCH-1
+    // lane 0 of the first loader wave takes the tiles; the others learn them
+    // from s_q after the next barrier
+    const bool taker = wave == NC && lane == 0;
+    const int64_t P = pair_count(a);
     auto stage = [&](int64_t t, int ch, uint32_t *slot) {
-        const int64_t seg = t / a.tiles_per_seg;
-        const TileCols c = tile_cols(a, t - seg * a.tiles_per_seg, lane);
+        const TileCols c = pair_cols(a, t, lane);
         const int j0 = ch * KC, jn = K - j0 < KC ? K - j0 : KC;
-        stage_inputs<NL, PER, true>(a, seg, c, slot, lane, lw, j0, jn, true);
+        stage_inputs<NL, PER, true>(a, 0, c, slot, lane, lw, j0, jn, true);
     };
-    int64_t tile = blockIdx.x;
+    if (taker) {
+        s_q[0] = take_tile(a, 0);
+        s_q[1] = take_tile(a, 1);
+    }
+    lds_barrier();
+    int64_t tile = s_q[0];  // tile of the item being computed
+    int64_t q1 = s_q[1];    // the tile to start after it
+    int taken = 2;
     int ch = 0;
-    if (loader && tile < a.total_tiles) stage(tile, 0, lds[0]);
+    if (loader && tile < P) stage(tile, 0, lds[0]);
     lds_barrier();
     int buf = 0;
     uint32_t acc[OPW][8];
-    while (tile < a.total_tiles) {
+    while (tile < P) {
         int64_t ntile = tile;
         int nch = ch + 1;
+        bool take = false;
         if (nch == NCH) {
             nch = 0;
-            ntile += gridDim.x;
+            ntile = q1;
+            take = ntile < P;  // q1 is consumed: take its successor (needed one item later)
         }
         if (loader) {
-            if (ntile < a.total_tiles) stage(ntile, nch, lds[buf ^ 1]);
+            int32_t got = 0;
+            if (take && taker) got = take_tile(a, taken);  // issued before the loads, its result waited on after them
+            if (ntile < P) stage(ntile, nch, lds[buf ^ 1]);
+            if (take && taker) s_q[taken & 3] = got;
         } else {
             if (ch == 0) {
 #pragma unroll
@@ -132,13 +155,13 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
                 }
             });
             if (ch == NCH - 1) {
-                const int64_t seg = tile / a.tiles_per_seg;
-                const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+                const TileCols c = pair_cols(a, tile, lane);
                 const int rbase = rbase_of(R, NC, wave), cnt = rows_of(R, NC, wave);
-                store_rows<OPW, true>(a, seg, c, rbase, cnt, acc);
+                store_rows<OPW, true>(a, 0, c, rbase, cnt, acc);
             }
         }
         lds_barrier();
+        if (take) q1 = s_q[taken & 3], taken++;
         buf ^= 1;
         tile = ntile;
         ch = nch;

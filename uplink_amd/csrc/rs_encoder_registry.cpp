@@ -282,7 +282,7 @@ const EncoderKernel *find_encoder(int k, int n, bool wait) {
 hipError_t launch_encode_special(const EncoderKernel &e, const RsArgs &args, int grid, hipStream_t s) {
     const bool parity_only = args.copy_off[0] < 0;
     const EncoderKernel::Variant &v = parity_only ? e.parity : e.full;
-    if (grid <= 0) grid = default_grid(args.total_tiles, v.wgs_per_cu);
+    if (grid <= 0) grid = default_grid((args.total_blocks + 1) / 2, v.wgs_per_cu);  // tiles = pairs of blocks
     RsArgs a = args;
     void *params[] = {&a};
     if (v.aot) return hipLaunchKernel(v.aot, dim3(grid), dim3(v.threads), params, 0, s);

@@ -138,6 +138,38 @@ __device__ __forceinline__ TileCols tile_cols(const RsArgs &a, int64_t tt, int l
     return c;
 }
 
+// The compile-time encoder's tile: two 1-KiB column blocks of the batch (64
+// chunks of 16 B of every share row), block t and block t + ceil(B / 2) of the
+// B blocks of all segments -- for a batch of segments, the same columns of
+// segments g and g + nseg/2.  A lane's 32 bytes are chunk `lane` of each.
+// Offsets are absolute (segment included).  Measured against two adjacent
+// blocks (one 2-KiB tile of one segment): the encode's 80 piece streams are
+// written at 5.6-6.5 instead of 4.5-4.7 TB/s (tools/exp/enc_shape_probe2.hip,
+// DESIGN.md §4).
+__device__ __forceinline__ void block_cols(const RsArgs &a, int64_t b, int lane, bool &v, int64_t &in, int64_t &out) {
+    v = false;
+    in = out = 0;
+    if (b >= a.total_blocks) return;
+    const uint32_t bps = (uint32_t)a.blocks_per_seg;
+    const uint32_t seg = (uint32_t)b / bps;
+    const int64_t q = (int64_t)((uint32_t)b - seg * bps) * 64 + lane;
+    if (q >= a.chunks_per_seg) return;
+    v = true;
+    const uint32_t cps = (uint32_t)a.cps;
+    const uint32_t s = (uint32_t)q / cps, t = (uint32_t)q - s * cps;
+    in = (int64_t)seg * a.in_seg_stride + (int64_t)s * a.in_stripe_stride + (int64_t)t * 16;
+    out = (int64_t)seg * a.out_seg_stride + (int64_t)s * a.out_stripe_stride + (int64_t)t * 16;
+}
+
+__device__ __forceinline__ int64_t pair_count(const RsArgs &a) { return (a.total_blocks + 1) >> 1; }
+
+__device__ __forceinline__ TileCols pair_cols(const RsArgs &a, int64_t t, int lane) {
+    TileCols c;
+    block_cols(a, t, lane, c.vA, c.inA, c.outA);
+    block_cols(a, t + pair_count(a), lane, c.vB, c.inB, c.outB);
+    return c;
+}
+
 // Phase A: inputs j0 .. j0+jn-1 (thread handles j = j0 + wave + NW*i), load
 // two 16-byte chunks, optionally copy them through (systematic shares),
 // bit-slice and write the planes to lds[(j-j0)*8 + p][lane].  All loads are
