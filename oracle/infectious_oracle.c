@@ -476,6 +476,49 @@ int or_decode(int k, int n, const uint8_t *enc, int ns, int *numbers, uint8_t **
     return or_rebuild(k, n, enc, ns, numbers, (const uint8_t **)data, len, out);
 }
 
+/* Decode as infectious runs it over whole share buffers (FEC.Correct: one
+ * syndrome row per share beyond k, accumulated with addmul over the whole
+ * buffer, Berlekamp-Welch only on the columns where a syndrome is non-zero;
+ * then Rebuild).  Same results as or_decode, whose per-column check is the
+ * plain restatement; this one is the CPU baseline of the reference benchmark's
+ * Decode (rs_test.go:616-631), not a checker of anything.
+ * Syndrome rows: with B the first k sorted shares and R the rest,
+ * H = [G_R G_B^-1 | I] annihilates every codeword restricted to B u R. */
+int or_decode_fast(int k, int n, const uint8_t *enc, int ns, int *numbers, uint8_t **data, size_t len, uint8_t *out) {
+    or_init();
+    if (ns < k) return -10;
+    sort_shares(ns, numbers, (const uint8_t **)data);
+    if (ns > k) {
+        uint8_t *gb = (uint8_t *)calloc((size_t)k * k, 1);
+        for (int i = 0; i < k; i++) memcpy(gb + (size_t)i * k, enc + (size_t)numbers[i] * k, k);
+        if (or_invert_matrix(gb, k) != 0) { free(gb); return -12; }
+        uint8_t *syn = (uint8_t *)malloc(len), *h = (uint8_t *)malloc(k), *cw = (uint8_t *)malloc(n),
+                *vals = (uint8_t *)malloc(ns);
+        int rc = 0;
+        for (int r = k; r < ns && rc == 0; r++) {
+            for (int b = 0; b < k; b++) {  /* h = G_r G_B^-1 */
+                uint8_t acc = 0;
+                for (int c = 0; c < k; c++) acc ^= gf_mul_table[enc[(size_t)numbers[r] * k + c]][gb[(size_t)c * k + b]];
+                h[b] = acc;
+            }
+            memcpy(syn, data[r], len);
+            for (int b = 0; b < k; b++) addmul(syn, data[b], h[b], len);
+            for (size_t col = 0; col < len && rc == 0; col++) {
+                if (!syn[col]) continue;
+                for (int i = 0; i < ns; i++) vals[i] = data[i][col];
+                rc = bw_column(k, n, ns, numbers, vals, cw);
+                if (rc == 0) {
+                    for (int i = 0; i < ns; i++) data[i][col] = cw[numbers[i]];
+                    /* later syndrome rows see the corrected column */
+                }
+            }
+        }
+        free(gb); free(syn); free(h); free(cw); free(vals);
+        if (rc) return rc;
+    }
+    return or_rebuild(k, n, enc, ns, numbers, (const uint8_t **)data, len, out);
+}
+
 /* ------------------------------------------------ reference-shaped baseline */
 /* Segment layout [stripe][k][ess]; pieces [n][nstripes*ess].
  * Per piece, per stripe EncodeSingle (segmentupload/encode.go:39-75): the

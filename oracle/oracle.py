@@ -51,6 +51,7 @@ def lib():
                                  ctypes.POINTER(u8p), ctypes.c_size_t, u8p]
         L.or_decode.argtypes = [ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(u8p), ctypes.c_size_t, u8p]
+        L.or_decode_fast.argtypes = L.or_decode.argtypes
         L.or_baseline_encode_segment.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, u8p,
                                                  ctypes.c_size_t, u8p, ctypes.c_int]
         L.or_baseline_rebuild_segment.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_int,
@@ -154,6 +155,20 @@ class FEC:
         ns, carr, parr, keep = self._shares_args(nums, [np.array(d, dtype=np.uint8) for d in datas])
         out = np.zeros(self.k * max(ln, 1), dtype=np.uint8)
         rc = lib().or_decode(self.k, self.n, _p(self.enc), ns, carr, parr, ln, _p(out))
+        if rc:
+            raise _err(rc)
+        return out[: self.k * ln]
+
+    def decode_fast(self, nums, datas) -> np.ndarray:
+        """Decode as infectious runs it on whole buffers (syndrome rows by addmul,
+        Berlekamp-Welch on flagged columns only): the CPU baseline of the
+        reference benchmark's Decode; same results as decode()."""
+        if not datas:
+            raise _err(-10)
+        ln = len(datas[0])
+        ns, carr, parr, keep = self._shares_args(nums, [np.array(d, dtype=np.uint8) for d in datas])
+        out = np.zeros(self.k * max(ln, 1), dtype=np.uint8)
+        rc = lib().or_decode_fast(self.k, self.n, _p(self.enc), ns, carr, parr, ln, _p(out))
         if rc:
             raise _err(rc)
         return out[: self.k * ln]

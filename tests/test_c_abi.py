@@ -36,3 +36,45 @@ def test_c_client_on_gpu_checked_library():
     assert "uplink_ec checked" not in r.stdout + r.stderr, r.stdout + r.stderr
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().splitlines()[-1].startswith("ok")
+
+
+BIN_EXIT = os.path.join(HERE, "c", "build", "exit_test")
+
+
+@pytest.mark.gpu
+def test_exit_while_encoder_compiles(tmp_path):
+    """main() returns while hiprtc compiles RS(11,23)'s encoder in the library's
+    background thread (tests/c/exit_test.c): exit waits for the
+    compile before the compiler library's destructors run, so the process
+    exits 0 with nothing on stderr (round 2: "double free or corruption")."""
+    assert os.path.exists(BIN_EXIT), "tests/c/build/exit_test missing: build() compiles it"
+    env = dict(os.environ, UPLINK_EC_JIT_CACHE=str(tmp_path / "jit"))
+    r = subprocess.run([BIN_EXIT, "11", "23"], capture_output=True, text=True, timeout=300, env=env)
+    # libdrm's note about its ids file is the driver stack's, not the library's
+    err = [ln for ln in r.stderr.splitlines() if "amdgpu.ids" not in ln]
+    assert r.returncode == 0 and not err, (r.returncode, r.stdout, r.stderr)
+    assert "while RS(11,23)'s encoder compiles" in r.stdout
+    # the compile that exit waited for finished and published its code object
+    cached = sorted(p.name for p in (tmp_path / "jit").iterdir())
+    assert any(n.endswith(".co") for n in cached) and any(n.endswith(".names") for n in cached), cached
+    assert (tmp_path / "jit").stat().st_mode & 0o077 == 0
+
+
+@pytest.mark.gpu
+def test_jit_cache_entry_with_a_bad_digest_is_recompiled(tmp_path):
+    """A cached code object that does not match the digest in its .names file
+    is removed and compiled again (the cache's code runs on the GPU)."""
+    env = dict(os.environ, UPLINK_EC_JIT_CACHE=str(tmp_path / "jit"))
+    r = subprocess.run([BIN_EXIT, "11", "23"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    co = [p for p in (tmp_path / "jit").iterdir() if p.name.endswith(".co")]
+    assert len(co) == 1
+    data = bytearray(co[0].read_bytes())
+    data[len(data) // 2] ^= 0xFF
+    co[0].write_bytes(bytes(data))
+    # the damaged entry is not used: the encoder is compiled again, so it is not ready
+    # at once and the client sees a compile in progress (exit_test's own check)
+    r = subprocess.run([BIN_EXIT, "11", "23"], capture_output=True, text=True, timeout=300, env=env)
+    err = [ln for ln in r.stderr.splitlines() if "amdgpu.ids" not in ln]
+    assert r.returncode == 0 and not err, (r.returncode, r.stdout, r.stderr)
+    assert co[0].read_bytes() != bytes(data), "the damaged code object was not replaced"

@@ -144,6 +144,35 @@ def test_decode_corrects_errors_berlekamp_welch(oracle):
     assert np.array_equal(f.decode([0, 2, 3, 6], [sh[i] for i in (0, 2, 3, 6)]), data)
 
 
+@pytest.mark.parametrize("k,n,ns,nbad", [(3, 7, 7, 2), (20, 50, 27, 3), (29, 80, 40, 5), (2, 4, 3, 0), (30, 60, 44, 7)])
+def test_decode_fast_matches_decode(oracle, k, n, ns, nbad):
+    """or_decode_fast (syndrome rows over whole buffers, the reference
+    benchmark's CPU baseline) returns what the per-column or_decode returns,
+    errors corrected in place the same way, on shuffled share subsets."""
+    f = oracle.FEC(k, n)
+    rng = np.random.default_rng(k * 1000 + ns)
+    ln = 333
+    data = rng.integers(0, 256, k * ln, dtype=np.uint8)
+    sh = f.encode(data)
+    nums = [int(x) for x in rng.permutation(n)[:ns]]
+    datas = [np.array(sh[i]) for i in nums]
+    for t in range(nbad):  # corrupt a few columns of a few shares (within e per column)
+        i = int(rng.integers(0, ns))
+        cols = rng.integers(0, ln, 9)
+        datas[i][cols] ^= rng.integers(1, 256, 9, dtype=np.uint8)
+    a = [d.copy() for d in datas]
+    b = [d.copy() for d in datas]
+    try:
+        want = f.decode(list(nums), a)
+    except oracle.OracleError as e:
+        with pytest.raises(oracle.OracleError, match=str(e).split(":")[0]):
+            f.decode_fast(list(nums), b)
+        return
+    assert np.array_equal(f.decode_fast(list(nums), b), want)
+    if nbad * 2 <= ns - k:
+        assert np.array_equal(want, data)
+
+
 @pytest.mark.parametrize("size,expected", [
     (0, 1024), (1, 1024), (1024 - 4, 1024), (1024, 1024),
     (32 * 1024 - 4, 16384), (32 * 1024, 17408), (32 * 1024 + 100, 17408)])

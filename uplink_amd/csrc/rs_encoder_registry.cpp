@@ -16,6 +16,7 @@
 
 #include <condition_variable>
 #include <cstdio>
+#include <dlfcn.h>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -72,7 +73,21 @@ std::string cache_dir() {
 
 void mkdirs(const std::string &path) {
     for (size_t i = 1; i <= path.size(); i++)
-        if (i == path.size() || path[i] == '/') (void)mkdir(path.substr(0, i).c_str(), 0755);
+        if (i == path.size() || path[i] == '/') (void)mkdir(path.substr(0, i).c_str(), 0700);
+}
+
+// The cache directory is trusted only if it is a directory (not a link) owned
+// by this user and writable by no one else: its code objects run on the GPU.
+bool cache_dir_trusted(const std::string &dir) {
+    struct stat st;
+    if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode)) return false;
+    return st.st_uid == geteuid() && (st.st_mode & (S_IWGRP | S_IWOTH)) == 0;
+}
+
+std::string hex64(uint64_t h) {
+    char hex[32];
+    snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
+    return hex;
 }
 
 struct JitEntry {
@@ -81,6 +96,7 @@ struct JitEntry {
     std::string full_name, parity_name;
     std::map<int, std::unique_ptr<EncoderKernel>> loaded;  // per device
     std::map<int, hipModule_t> modules;
+    bool recompiled = false;  // compiled again after a cached code object failed to load
 };
 
 std::mutex g_mu;
@@ -90,11 +106,18 @@ std::vector<std::thread> g_threads;  // compile threads (joined at exit)
 std::mutex g_compile_mu;             // one compilation at a time
 bool g_exiting = false;              // set at exit: queued compilations are skipped
 
-// Compile threads still running when the process exits must finish before the
-// HIP runtime tears itself down: the runtime registers its exit handler on its
-// first use, so this one, registered at the first compile (always later),
-// runs before it.  Only the compilation in progress is waited for; the ones
-// queued behind it give up (each takes seconds to a minute).
+// Compile threads still running when the process exits must finish before
+// anything they use is torn down.  exit() runs the handlers and C++ static
+// destructors in the reverse order of their registration.  The HIP runtime
+// registers its own on its first use, before any compile.  The compiler
+// library (comgr, which hiprtc dlopens on its first compile) registers its
+// static destructors when it is loaded: loaded lazily inside the compile
+// thread, that was AFTER this handler, so at exit comgr's LLVM state was
+// destroyed under a running compile -- the "double free or corruption (!prev)"
+// abort of round 2.  So comgr is loaded here first
+// (load_compiler), and this handler, registered after it, runs before its
+// destructors.  Only the compilation in progress is waited for; the ones queued
+// behind it give up (each takes seconds to a minute).
 void join_compiles() {
     std::vector<std::thread> t;
     {
@@ -106,13 +129,20 @@ void join_compiles() {
         if (th.joinable()) th.join();
 }
 
+// Load the compiler library hiprtc would load on its first compile, and keep it
+// (RTLD_NODELETE), so that its destructors are registered before join_compiles.
+void load_compiler() {
+    for (const char *so : {"libamd_comgr.so.3", "libamd_comgr.so"})
+        if (dlopen(so, RTLD_NOW | RTLD_GLOBAL | RTLD_NODELETE)) return;
+}
+
 std::string variant_expr(int k, int n, int nc, int nl) {
     return "&uplink_ec::enc::rs_encode_special<" + std::to_string(k) + ", " + std::to_string(n) + ", " +
            std::to_string(nc) + ", " + std::to_string(nl) + ">";
 }
 
 // Compile (or read from the cache) the two variants of (k, n) for `arch`.
-void compile_entry(JitEntry *e, std::string arch, int k, int n) {
+void compile_entry(JitEntry *e, std::string arch, int k, int n, bool read_cache) {
     std::lock_guard<std::mutex> serial(g_compile_mu);
     {
         std::lock_guard<std::mutex> g(g_mu);
@@ -135,16 +165,24 @@ void compile_entry(JitEntry *e, std::string arch, int k, int n) {
     (void)hiprtcVersion(&ver_major, &ver_minor);
     h = fnv1a(h, &ver_major, sizeof ver_major);
     h = fnv1a(h, &ver_minor, sizeof ver_minor);
-    char hex[32];
-    snprintf(hex, sizeof hex, "%016llx", (unsigned long long)h);
-    const std::string dir = cache_dir(), path = dir + "/enc_" + std::to_string(k) + "_" + std::to_string(n) + "_" + hex;
+    const std::string dir = cache_dir(), path = dir + "/enc_" + std::to_string(k) + "_" + std::to_string(n) + "_" + hex64(h);
+    mkdirs(dir);
+    const bool trusted = cache_dir_trusted(dir);
     std::vector<char> code;
     std::string names[2];
-    {
+    if (trusted && read_cache) {
+        // .names holds the two kernel names and the digest of the code object; an
+        // entry that does not match it is removed and compiled again
         std::ifstream in(path + ".co", std::ios::binary);
         std::ifstream nm(path + ".names");
-        if (in && nm && std::getline(nm, names[0]) && std::getline(nm, names[1]))
+        std::string digest;
+        if (in && nm && std::getline(nm, names[0]) && std::getline(nm, names[1]) && std::getline(nm, digest))
             code.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+        if (!code.empty() && hex64(fnv1a(0xcbf29ce484222325ull, code.data(), code.size())) != digest) code.clear();
+        if (code.empty()) {
+            (void)remove((path + ".co").c_str());
+            (void)remove((path + ".names").c_str());
+        }
     }
     if (code.empty()) {
         hiprtcProgram prog;
@@ -181,13 +219,12 @@ void compile_entry(JitEntry *e, std::string arch, int k, int n) {
             hiprtcDestroyProgram(&prog);
         }
         if (!ok) code.clear();
-        if (!code.empty()) {  // publish atomically: write a temp file, rename
-            mkdirs(dir);
+        if (!code.empty() && trusted) {  // publish atomically: write a temp file, rename
             const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
             std::ofstream out(tmp + ".co", std::ios::binary);
             out.write(code.data(), (std::streamsize)code.size());
             std::ofstream nm(tmp + ".names");
-            nm << names[0] << "\n" << names[1] << "\n";
+            nm << names[0] << "\n" << names[1] << "\n" << hex64(fnv1a(0xcbf29ce484222325ull, code.data(), code.size())) << "\n";
             out.close();
             nm.close();
             if (out && nm) {
@@ -235,8 +272,11 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
         JitEntry *e = new JitEntry();
         g_jit.emplace(key, std::unique_ptr<JitEntry>(e));
         static std::once_flag once;
-        std::call_once(once, [] { std::atexit(join_compiles); });
-        g_threads.emplace_back(compile_entry, e, arch, k, n);
+        std::call_once(once, [] {
+            load_compiler();
+            std::atexit(join_compiles);
+        });
+        g_threads.emplace_back(compile_entry, e, arch, k, n, true);
         it = g_jit.find(key);
     }
     JitEntry *e = it->second.get();
@@ -249,6 +289,20 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
     if (hipModuleLoadData(&mod, e->code.data()) != hipSuccess ||
         hipModuleGetFunction(&f_full, mod, e->full_name.c_str()) != hipSuccess ||
         hipModuleGetFunction(&f_par, mod, e->parity_name.c_str()) != hipSuccess) {
+        if (mod) (void)hipModuleUnload(mod);
+        if (!e->recompiled && !g_exiting) {
+            // a code object that passed its digest but does not load (another
+            // driver, a damaged entry): compiled again once, without the cache
+            e->recompiled = true;
+            e->state = JitEntry::kCompiling;
+            g_threads.emplace_back(compile_entry, e, arch, k, n, false);
+            if (!wait) return nullptr;
+            g_cv.wait(g, [&] { return e->state != JitEntry::kCompiling; });
+            if (e->state == JitEntry::kReady) {
+                g.unlock();
+                return jit_encoder(k, n, false);
+            }
+        }
         fprintf(stderr, "uplink_ec: loading the RS(%d,%d) encoder failed\n", k, n);
         e->state = JitEntry::kFailed;
         return nullptr;
