@@ -52,6 +52,11 @@ PIECE = NSTRIPES * ESS  # 2,314,240
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+# the library's RS(29,80) encoders as rocprofv3 names them (rs_encoder.hpp: 8 compute + 4
+# loader waves; the last argument tells the full encode from the parity-only one)
+ENC_FULL_KERNEL = "rs_encode_special<29, 80, 8, 4, true>"
+ENC_PARITY_KERNEL = "rs_encode_special<29, 80, 8, 4, false>"
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +270,60 @@ def other_configs(L, dev, sptr, reps: int = 10):
     return out
 
 
+def decode_with_detection(L, dev, sptr, reps: int = 4, nb: int = 16):
+    """Informational, outside the timed region: Decode with error detection on
+    whole RS(29,80) 64 MiB segments, nb per call (ec_decode_segments_batched:
+    syndrome rows checked for zero in the kernel, then Rebuild) from
+    k+1 .. k+n/4 clean shares in shuffled order, the reference benchmark's
+    Decode shape (private/eestream/rs_test.go:616-631) at segment size.  Per
+    extra-share count: wall time per segment (synchronous: the check's outcome
+    is read back) and HBM fraction of the algorithmic bytes (the ns pieces
+    read + the segment written)."""
+    ctx = ctypes.c_void_p()
+    if L.ec_create(K, N, ESS, ctypes.byref(ctx)):
+        return {}
+    nstripes = (RAW_SEGMENT + 4 + K * ESS - 1) // (K * ESS)
+    spad, plen = nstripes * K * ESS, nstripes * ESS
+    segs = torch.randint(0, 256, (nb, spad), dtype=torch.uint8, device=dev)
+    pcs = torch.empty((nb, N, plen), dtype=torch.uint8, device=dev)
+    assert L.ec_encode_segments(ctx, segs.data_ptr(), nb, nstripes, pcs.data_ptr(), 0, sptr) == 0
+    back = torch.empty_like(segs)
+    rng = np.random.default_rng(616)
+    res = {}
+    ok = True
+    for extra in (1, 4, 10, 20):
+        sets = [[int(x) for x in rng.permutation(N)[:K + extra]] for _ in range(4)]
+        args = [((ctypes.c_int * len(s))(*s), (ctypes.c_void_p * len(s))(*[pcs.data_ptr() + i * plen for i in s]))
+                for s in sets]
+
+        def call(i):
+            nums, ptrs = args[i % len(args)]
+            rc = L.ec_decode_segments_batched(ctx, K + extra, nums, ptrs, nstripes, nb, N * plen, spad,
+                                              back.data_ptr(), sptr)
+            assert rc == 0, _native.strerror(rc)
+        for i in range(len(args)):  # plans made, outputs checked
+            back.fill_(0)
+            call(i)
+            torch.cuda.synchronize()
+            ok = ok and bool(torch.equal(back, segs))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(reps * len(args)):
+            call(i)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / (reps * len(args) * nb)
+        alg = plen * (K + extra) + spad
+        res[f"k+{extra}"] = {"us_per_segment": round(wall * 1e6, 2), "GBps": round(alg / wall / 1e9, 1),
+                             "frac": round(alg / wall / 1e9 / HBM_PEAK_GBPS, 4),
+                             "data_GiBps": round(spad / wall / 2**30, 1)}
+    res["verified"] = ok
+    res["note"] = (f"clean shares, {nb} segments per call, wall clock per call (launch, check read-back and sync "
+                   "included); 4 seeded share sets per count, plans warm; informational, not in value")
+    del segs, pcs, back
+    L.ec_destroy(ctx)
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -284,7 +343,7 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    L = _native.load(args.lib) if args.lib else _native.load()
+    L = _native.load(args.lib, partial=True) if args.lib else _native.load()
     if L.ec_set_device(torch.cuda.current_device()) != 0:
         raise RuntimeError("ec_set_device failed")
     ctx = ctypes.c_void_p()
@@ -449,7 +508,7 @@ def main():
     dec_gbps = dec_bytes / t_dec_full / 1e9
     enc_name = L.ec_encode_kernel_name(ctx).decode()
     kernels = {
-        "encode": {"kernel": ("rs_encode_special<29,80,4,4> (special)" if enc_name == "special"
+        "encode": {"kernel": (f"{ENC_FULL_KERNEL} (special)" if enc_name == "special"
                               else f"rs_matmul_jt<7, true> ({enc_name})"), "avg_us": round(t_enc_full * 1e6, 2),
                    "bytes_per_launch": int(enc_bytes), "achieved_GBps": round(enc_gbps, 1)},
         "decode": {"kernel": ("rs_matmul_jt<NW, true> (straight-line body)"
@@ -464,7 +523,7 @@ def main():
     par_bytes = B * S_PAD * (1 + (N - K) / K)
     par_frac = round(par_bytes / t_par / 1e9 / HBM_PEAK_GBPS, 4)
     kernels["encode_parity_only"] = {
-        "kernel": ("rs_encode_special<29,80,8,4>" if enc_name == "special" else "rs_matmul_jt<7, true>")
+        "kernel": (ENC_PARITY_KERNEL if enc_name == "special" else "rs_matmul_jt<7, true>")
                   + " (EC_FLAG_PARITY_ONLY)", "avg_us": round(t_par * 1e6, 2),
         "avg_us_back_to_back": round(t_par_b2b * 1e6, 2),
         "bytes_per_launch": int(par_bytes), "achieved_GBps": round(par_bytes / t_par / 1e9, 1),
@@ -538,6 +597,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_other_configs:
         line["other_configs"] = other_configs(L, dev, sptr)
+        if hasattr(L, "ec_decode_segments_batched"):  # (an older --lib build lacks it)
+            line["other_configs"]["RS(29,80) decode with error detection"] = decode_with_detection(L, dev, sptr)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample_s)
     if rank == 0:

@@ -126,6 +126,23 @@ int ec_rebuild_segments(const ec_ctx *ctx, int nshares, const int *nums, const u
 int ec_rebuild_segments_batched(const ec_ctx *ctx, int nshares, const int *nums, const uint8_t *const *pieces,
                                 size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
                                 uint8_t *out, ec_stream stream);
+/* Decode whole segments with error detection: FEC.Decode (Correct +
+ * Rebuild) on every stripe of the pieces at once -- what StripeReader runs
+ * per stripe when error detection is on (private/eestream/stripe.go:407-408
+ * -> rsScheme.Decode, rs.go:32-38).  Same arguments as ec_rebuild_segments;
+ * with nshares > k every column is checked against the code (syndrome rows
+ * computed and tested for zero inside the kernel, nothing stored) and, where
+ * a column is not a codeword, corrected by Berlekamp-Welch.  Corrected
+ * shares are written back into the caller's pieces, as infectious corrects
+ * share.Data in place.  Returns when done (the check's outcome is read back):
+ * EC_ERR_TOO_MANY_ERRORS / EC_ERR_NOT_ENOUGH_SHARES as Decode returns them. */
+int ec_decode_segments(const ec_ctx *ctx, int nshares, const int *nums, uint8_t *const *pieces, size_t nstripes,
+                       uint8_t *out, ec_stream stream);
+/* The same over nseg segments in one check and one rebuild launch (strides as
+ * ec_rebuild_segments_batched); a segment with errors is corrected on its own. */
+int ec_decode_segments_batched(const ec_ctx *ctx, int nshares, const int *nums, uint8_t *const *pieces,
+                               size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
+                               uint8_t *out, ec_stream stream);
 
 /* ---- host-memory pipeline (end-to-end path, PCIe-inclusive) ----
  * Same layouts as the device calls, but in host memory (pinned memory from

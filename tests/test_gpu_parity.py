@@ -792,3 +792,105 @@ def test_prepare_encoder_reports_limits():
     assert _kernel_name(s3) == "generic"
     s2 = scheme(29, 80, 256)
     assert s2._lib.ec_prepare_encoder(s2._ctx, 0) == 1
+
+
+# ---- whole-segment Decode with error detection (ec_decode_segments) -----------
+
+def gpu_decode_segments(sch, d_pieces, nums, stripes):
+    k, ess = sch.fc.k, sch.ess
+    plen = stripes * ess
+    base = d_pieces.data_ptr()
+    out = torch.full((stripes * k * ess,), 0xCD, dtype=torch.uint8, device="cuda")
+    eestream.SegmentCodec(sch).decode_segments(nums, [base + i * plen for i in nums], stripes, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("k,n,ess,stripes,extras", [
+    (29, 80, 256, 9040, (1, 4, 20)),     # the production segment, k+1 .. k+n/4 shares
+    (20, 50, 1024, 41, (1, 12)), (30, 60, 256, 130, (2, 15)), (50, 80, 256, 33, (3, 20)), (2, 4, 1024, 7, (1, 2)),
+    (4, 10, 256, 1025, (6,)), (3, 5, 100, 4, (2,)),   # ess % 16 != 0: the workspace path
+])
+def test_decode_segments_clean(oracle, k, n, ess, stripes, extras):
+    """Clean pieces, more than k of them in any order: the syndrome check
+    finds nothing and the output is the segment (the reference benchmark's
+    Decode shape, rs_test.go:616-631, on whole segments)."""
+    rng = np.random.default_rng(k * 31 + n + stripes)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    d_pieces = torch.from_numpy(ref).cuda().reshape(1, n, -1)
+    for extra in extras:
+        nums = [int(x) for x in rng.permutation(n)[:k + extra]]
+        assert np.array_equal(gpu_decode_segments(sch, d_pieces, nums, stripes), seg), (k, n, extra)
+    assert np.array_equal(d_pieces.cpu().numpy()[0], ref)  # clean pieces are left as they are
+
+
+@pytest.mark.parametrize("case", ["one bad piece", "scattered", "bad piece + scattered", "too many", "k+1 with error"])
+def test_decode_segments_corrects_like_the_oracle(oracle, case):
+    """Corrupted pieces through ec_decode_segments: the output and the
+    corrected pieces match the oracle's Decode of the same shares (per-stripe
+    infectious semantics: Berlekamp-Welch per byte column), and the error
+    cases raise what Decode raises."""
+    k, n, ess, stripes = 29, 80, 256, 300
+    rng = np.random.default_rng(hash(case) % 1000)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    sch = scheme(k, n, ess)
+    f = oracle.FEC(k, n)
+    ref = f.encode_segment(seg, ess, threads=8)
+    extra = 1 if case == "k+1 with error" else 8
+    nums = [int(x) for x in rng.permutation(n)[:k + extra]]
+    recv = ref.copy()
+    plen = stripes * ess
+    if case in ("one bad piece", "bad piece + scattered", "too many"):
+        recv[nums[3]] ^= rng.integers(1, 256, plen, dtype=np.uint8)
+    if case in ("scattered", "bad piece + scattered", "k+1 with error"):
+        for t in range(3):
+            where = rng.choice(plen, 50, replace=False)
+            recv[nums[10 + t]][where] ^= rng.integers(1, 256, 50, dtype=np.uint8)
+    if case == "too many":  # 5 > e = 4 bad pieces
+        for i in (5, 7, 9, 11):
+            recv[nums[i]] ^= rng.integers(1, 256, plen, dtype=np.uint8)
+    d_pieces = torch.from_numpy(recv).cuda().reshape(1, n, -1)
+    if case in ("too many", "k+1 with error"):
+        with pytest.raises(eestream.InfectiousError):
+            gpu_decode_segments(sch, d_pieces, nums, stripes)
+        with pytest.raises(oracle.OracleError):
+            f.decode(sorted(nums), [recv[i].copy() for i in sorted(nums)])
+        return
+    got = gpu_decode_segments(sch, d_pieces, nums, stripes)
+    assert np.array_equal(got, seg)
+    fixed = d_pieces.cpu().numpy()[0]
+    for i in nums:  # corrected in place
+        assert np.array_equal(fixed[i], ref[i]), i
+    # the oracle decodes the same received shares to the same bytes: as one long share
+    # per piece (columns are independent codewords), its output is the k data pieces
+    sn = sorted(nums)
+    want = f.decode(sn, [recv[i].copy() for i in sn]).reshape(k, plen)
+    assert np.array_equal(want, ref[:k])
+
+
+def test_decode_segments_batched(oracle):
+    """Several segments per call (one check and one rebuild launch): clean
+    segments decode; a segment with a bad piece among clean ones is corrected
+    on its own, the others untouched."""
+    k, n, ess, stripes, nseg = 29, 80, 256, 200, 4
+    rng = np.random.default_rng(99)
+    sch = scheme(k, n, ess)
+    f = oracle.FEC(k, n)
+    segs = rng.integers(0, 256, (nseg, stripes * k * ess), dtype=np.uint8)
+    refs = np.stack([f.encode_segment(s, ess, threads=8) for s in segs])
+    plen = stripes * ess
+    nums = [int(x) for x in rng.permutation(n)[:k + 6]]
+    for bad_seg in (None, 2):
+        recv = refs.copy()
+        if bad_seg is not None:
+            recv[bad_seg, nums[4]] ^= rng.integers(1, 256, plen, dtype=np.uint8)
+        d_pieces = torch.from_numpy(recv).cuda()
+        out = torch.zeros((nseg, stripes * k * ess), dtype=torch.uint8, device="cuda")
+        base = d_pieces.data_ptr()
+        eestream.SegmentCodec(sch).decode_segments(nums, [base + i * plen for i in nums], stripes, out, nseg=nseg,
+                                                   piece_seg_stride=n * plen, out_seg_stride=stripes * k * ess)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), segs)
+        assert np.array_equal(d_pieces.cpu().numpy(), refs)  # the bad piece corrected in place

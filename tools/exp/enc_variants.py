@@ -27,6 +27,8 @@ RAW = 64 << 20
 def load(path):
     lib = ctypes.CDLL(path)
     for name, (res, args) in _native.SIGNATURES.items():
+        if not hasattr(lib, name):  # an older build for the A/B
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

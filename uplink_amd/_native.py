@@ -55,6 +55,11 @@ SIGNATURES = {
     "ec_encode_segments": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, ctypes.c_int, vp]),
     "ec_rebuild_segments": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
                                            ctypes.c_size_t, vp, vp]),
+    "ec_decode_segments": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                          ctypes.c_size_t, vp, vp]),
+    "ec_decode_segments_batched": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                                  ctypes.c_size_t, ctypes.c_size_t, ctypes.c_longlong,
+                                                  ctypes.c_longlong, vp, vp]),
     "ec_rebuild_segments_batched": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_size_t,
                                                    ctypes.c_longlong, ctypes.c_longlong, vp, vp]),
@@ -98,8 +103,10 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH):
-    """Load libuplink_ec.so; raises if it is absent (no silent fallback)."""
+def load(path: str = LIB_PATH, partial: bool = False):
+    """Load libuplink_ec.so; raises if it is absent (no silent fallback).
+    partial: an older build for an A/B (tools/exp, bench.py --lib) may lack
+    later exports; those are left unbound instead of failing the load."""
     global _lib
     if _lib is not None:
         return _lib
@@ -117,6 +124,8 @@ def load(path: str = LIB_PATH):
             f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if partial and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

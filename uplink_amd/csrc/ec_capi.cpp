@@ -335,7 +335,7 @@ int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int 
 
 // Cached plan for `key`, built from make_matrix() on a miss.
 template <typename F>
-int cached_plan(ec_ctx *c, const std::vector<int> &key, F &&make_matrix, PlanPtr *out) {
+int cached_plan(ec_ctx *c, const std::vector<int> &key, F &&make_matrix, PlanPtr *out, int nin = -1) {
     {
         std::lock_guard<std::mutex> g(c->mu);
         for (auto it = c->plans.begin(); it != c->plans.end(); ++it) {
@@ -352,7 +352,7 @@ int cached_plan(ec_ctx *c, const std::vector<int> &key, F &&make_matrix, PlanPtr
     int rc = make_matrix(M, rows, missing);
     if (rc) return rc;
     PlanPtr p;
-    rc = build_plan(c, key, M.data(), rows, c->k, &p);
+    rc = build_plan(c, key, M.data(), rows, nin < 0 ? c->k : nin, &p);
     if (rc) return rc;
     p->missing = std::move(missing);
     std::vector<PlanPtr> evicted;
@@ -1445,6 +1445,129 @@ static int reencode(ec_ctx *c, const uint8_t *d, size_t slot, size_t len, const 
     return run_matmul(c, a, out_off.data(), *plan, 1, bits, st);
 }
 
+// Where the Correct step keeps its data in a device workspace of ns share
+// slots `slot` bytes apart (ec_decode, and ec_decode_segments' error path).
+struct CorrectLayout {
+    size_t slot, exp_at, flags_at, cols_at, nums_at, stat_at, out_at, samp_at, bytes;
+    static constexpr int kSample = 64;  // flagged columns decoded first to locate bad shares
+    CorrectLayout(size_t share_len, int nshares, int k, size_t out_bytes) {
+        slot = (share_len + 15) & ~(size_t)15;
+        const int extra = nshares - k;
+        exp_at = slot * nshares;
+        flags_at = exp_at + slot * (size_t)extra;
+        cols_at = (flags_at + slot + 15) & ~(size_t)15;
+        nums_at = cols_at + share_len * 8;
+        stat_at = nums_at + 4 * 256;
+        out_at = (stat_at + share_len * 4 + 15) & ~(size_t)15;
+        samp_at = (out_at + out_bytes + 15) & ~(size_t)15;  // sample cols, status, changed, row lists
+        bytes = samp_at + kSample * (8 + 4 + (size_t)nshares) + 8 * (size_t)nshares + 64;
+    }
+};
+
+// FEC.Correct on the nshares shares in the workspace (slots L.slot apart, sorted
+// by number): re-encode the shares beyond the first k from the first k and flag
+// the columns where any differs; correct those (a bad piece's columns by the
+// fast path below, the rest by Berlekamp-Welch), in place.  *changed: whether
+// any column was flagged (the shares were rewritten).
+static int correct_device(ec_ctx *c, uint8_t *d, const CorrectLayout &L, size_t share_len, const int *nums,
+                          int nshares, hipStream_t st, bool *changed) {
+    const int k = c->k, extra = nshares - k;
+    constexpr int kSample = CorrectLayout::kSample;
+    const size_t slot = L.slot;
+    *changed = false;
+    if (extra <= 0 || share_len == 0) return EC_OK;
+    auto bw_columns = [&](const std::vector<int64_t> &cl) -> int {  // Berlekamp-Welch on columns, in place
+        if (cl.empty()) return EC_OK;
+        if (hipMemcpyAsync(d + L.cols_at, cl.data(), cl.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+            launch_berlekamp_welch(d, slot, (int64_t)share_len, (const int *)(d + L.nums_at), k, c->n, nshares,
+                                   (const int64_t *)(d + L.cols_at), (int)cl.size(), (int *)(d + L.stat_at), st) !=
+                hipSuccess)
+            return EC_ERR_DEVICE;
+        std::vector<int> status(cl.size());
+        if (hipMemcpyAsync(status.data(), d + L.stat_at, 4 * cl.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return EC_ERR_DEVICE;
+        for (int s2 : status) {
+            if (s2 == -6) return EC_ERR_NOT_ENOUGH_SHARES;
+            if (s2 == -7) return EC_ERR_TOO_MANY_ERRORS;
+            if (s2 != 0) return EC_ERR_UNSUPPORTED;
+        }
+        return EC_OK;
+    };
+    std::vector<int> basis(k), rest(extra);
+    for (int i = 0; i < k; i++) basis[i] = i;
+    for (int r = 0; r < extra; r++) rest[r] = k + r;
+    int rc = reencode(c, d, slot, share_len, nums, basis.data(), rest.data(), extra, d + L.exp_at, st);
+    if (rc) return rc;
+    if (launch_flag_columns(d, slot, d + L.exp_at, slot, k, nshares, share_len, d + L.flags_at, st) != hipSuccess)
+        return EC_ERR_DEVICE;
+    std::vector<uint8_t> flags(share_len);
+    if (hipMemcpyAsync(flags.data(), d + L.flags_at, share_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(d + L.nums_at, nums, 4 * (size_t)nshares, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return EC_ERR_DEVICE;
+    std::vector<int64_t> cols;
+    for (size_t col = 0; col < share_len; col++)
+        if (flags[col]) cols.push_back((int64_t)col);
+    if (cols.empty()) return EC_OK;
+    *changed = true;
+    // Fast path for errors confined to a few shares (a bad piece): decode a sample of the
+    // flagged columns, take the shares BW rewrote there as the bad set B, and if
+    // |B| <= e check every column on the other shares alone.  Where they agree, the
+    // codeword they define is within e of what was received, so it is the unique BW
+    // answer: B is rewritten from them.  Only columns where they disagree go to BW.
+    const int e = extra / 2;
+    if (e >= 1 && cols.size() > (size_t)4 * kSample) {
+        std::vector<int64_t> samp(kSample);
+        for (int i = 0; i < kSample; i++) samp[i] = cols[(size_t)i * cols.size() / kSample];
+        uint8_t *d_changed = d + L.samp_at + kSample * 12;
+        if (hipMemcpyAsync(d + L.samp_at, samp.data(), kSample * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+            launch_berlekamp_welch(d, slot, (int64_t)share_len, (const int *)(d + L.nums_at), k, c->n, nshares,
+                                   (const int64_t *)(d + L.samp_at), kSample, (int *)(d + L.samp_at + kSample * 8),
+                                   st, d_changed) != hipSuccess)
+            return EC_ERR_DEVICE;
+        std::vector<int> sstat(kSample);
+        std::vector<uint8_t> chg((size_t)kSample * nshares);
+        if (hipMemcpyAsync(sstat.data(), d + L.samp_at + kSample * 8, 4 * kSample, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(chg.data(), d_changed, chg.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return EC_ERR_DEVICE;
+        bool sample_ok = true;
+        for (int s2 : sstat) sample_ok = sample_ok && s2 == 0;
+        std::vector<int> bad, good;
+        for (int i = 0; i < nshares; i++) {
+            bool b = false;
+            for (int t = 0; t < kSample && sample_ok; t++) b = b || chg[(size_t)t * nshares + i];
+            (b ? bad : good).push_back(i);
+        }
+        if (sample_ok && !bad.empty() && (int)bad.size() <= e && (int)good.size() >= k) {
+            // expected rows: the other good shares, then the bad ones, from the first k good
+            std::vector<int> outs(good.begin() + k, good.end());
+            const int ncheck = (int)outs.size();
+            outs.insert(outs.end(), bad.begin(), bad.end());
+            int *d_rows = (int *)(d_changed + chg.size() + 16 - (chg.size() % 16));
+            rc = reencode(c, d, slot, share_len, nums, good.data(), outs.data(), (int)outs.size(), d + L.exp_at, st);
+            if (rc) return rc;
+            if (hipMemcpyAsync(d_rows, outs.data(), 4 * outs.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+                launch_flag_rows(d, slot, d_rows, ncheck, d + L.exp_at, slot, share_len, d + L.flags_at, st) != hipSuccess ||
+                hipMemcpyAsync(flags.data(), d + L.flags_at, share_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return EC_ERR_DEVICE;
+            std::vector<int64_t> rest_cols;
+            for (size_t col = 0; col < share_len; col++)
+                if (flags[col]) rest_cols.push_back((int64_t)col);
+            // rewrite the bad shares where the good ones agree, then BW the rest on the
+            // received data (the sample columns are already decoded: their good
+            // shares agree now)
+            if (launch_put_rows(d, slot, d_rows + ncheck, (int)bad.size(), d + L.exp_at + slot * ncheck, slot,
+                                share_len, d + L.flags_at, st) != hipSuccess)
+                return EC_ERR_DEVICE;
+            return bw_columns(rest_cols);
+        }
+    }
+    return bw_columns(cols);
+}
+
 int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t share_len, uint8_t *out) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!c || (nshares > 0 && (!nums || !shares))) return EC_ERR_INVALID_ARG;
@@ -1457,133 +1580,162 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
     for (int i = 0; i < nshares; i++)
         if (nums[i] < 0 || nums[i] >= c->n) return EC_ERR_INVALID_SHARE;
     if (k > kMaxOps || nshares - k > kMaxOps) return EC_ERR_UNSUPPORTED;
-    const size_t slot = (share_len + 15) & ~(size_t)15;
-    const int extra = nshares - k;
-    constexpr int kSample = 64;  // flagged columns decoded first to locate bad shares
-    const size_t exp_at = slot * nshares;
-    const size_t flags_at = exp_at + slot * (size_t)extra;
-    const size_t cols_at = (flags_at + slot + 15) & ~(size_t)15;
-    const size_t nums_at = cols_at + share_len * 8;
-    const size_t stat_at = nums_at + 4 * 256;
-    const size_t out_at = (stat_at + share_len * 4 + 15) & ~(size_t)15;
-    const size_t samp_at = (out_at + share_len * k + 15) & ~(size_t)15;  // sample cols, status, changed, row lists
-    const size_t samp_bytes = kSample * (8 + 4 + (size_t)nshares) + 8 * (size_t)nshares + 64;
-    Workspace *w = acquire_ws(c, samp_at + samp_bytes);
+    const CorrectLayout L(share_len, nshares, k, share_len * k);
+    Workspace *w = acquire_ws(c, L.bytes);
     if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
     int rc = EC_OK;
     uint8_t *d = w->d_buf;
     hipStream_t st = w->stream;
-    auto bw_columns = [&](const std::vector<int64_t> &cl) -> int {  // Berlekamp-Welch on columns, in place
-        if (cl.empty()) return EC_OK;
-        if (hipMemcpyAsync(d + cols_at, cl.data(), cl.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-            launch_berlekamp_welch(d, slot, (int64_t)share_len, (const int *)(d + nums_at), k, c->n, nshares,
-                                   (const int64_t *)(d + cols_at), (int)cl.size(), (int *)(d + stat_at), st) !=
-                hipSuccess)
-            return EC_ERR_DEVICE;
-        std::vector<int> status(cl.size());
-        if (hipMemcpyAsync(status.data(), d + stat_at, 4 * cl.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return EC_ERR_DEVICE;
-        for (int s2 : status) {
-            if (s2 == -6) return EC_ERR_NOT_ENOUGH_SHARES;
-            if (s2 == -7) return EC_ERR_TOO_MANY_ERRORS;
-            if (s2 != 0) return EC_ERR_UNSUPPORTED;
-        }
-        return EC_OK;
-    };
     do {
         for (int i = 0; i < nshares; i++)
-            if (hipMemcpyAsync(d + slot * i, shares[i], share_len, hipMemcpyHostToDevice, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+            if (hipMemcpyAsync(d + L.slot * i, shares[i], share_len, hipMemcpyHostToDevice, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         if (rc) break;
-        if (extra > 0) {
-            // Correct: re-encode the shares beyond the first k from the first k and flag the
-            // columns where any differs
-            std::vector<int> basis(k), rest(extra);
-            for (int i = 0; i < k; i++) basis[i] = i;
-            for (int r = 0; r < extra; r++) rest[r] = k + r;
-            rc = reencode(c, d, slot, share_len, nums, basis.data(), rest.data(), extra, d + exp_at, st);
+        bool changed = false;
+        rc = correct_device(c, d, L, share_len, nums, nshares, st, &changed);
+        if (rc) break;
+        if (changed) {  // infectious corrects share.Data in place
+            for (int i = 0; i < nshares; i++)
+                if (hipMemcpyAsync(shares[i], d + L.slot * i, share_len, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
             if (rc) break;
-            if (launch_flag_columns(d, slot, d + exp_at, slot, k, nshares, share_len, d + flags_at, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-            std::vector<uint8_t> flags(share_len);
-            if (hipMemcpyAsync(flags.data(), d + flags_at, share_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(d + nums_at, nums, 4 * (size_t)nshares, hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-            std::vector<int64_t> cols;
-            for (size_t col = 0; col < share_len; col++)
-                if (flags[col]) cols.push_back((int64_t)col);
-            if (!cols.empty()) {
-                // Fast path for errors confined to a few shares (a bad piece): decode a sample of the
-                // flagged columns, take the shares BW rewrote there as the bad set B, and if
-                // |B| <= e check every column on the other shares alone.  Where they agree, the
-                // codeword they define is within e of what was received, so it is the unique BW
-                // answer: B is rewritten from them.  Only columns where they disagree go to BW.
-                bool done = false;
-                const int e = extra / 2;
-                if (e >= 1 && cols.size() > (size_t)4 * kSample) {
-                    std::vector<int64_t> samp(kSample);
-                    for (int i = 0; i < kSample; i++) samp[i] = cols[(size_t)i * cols.size() / kSample];
-                    uint8_t *d_changed = d + samp_at + kSample * 12;
-                    if (hipMemcpyAsync(d + samp_at, samp.data(), kSample * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        launch_berlekamp_welch(d, slot, (int64_t)share_len, (const int *)(d + nums_at), k, c->n, nshares,
-                                               (const int64_t *)(d + samp_at), kSample, (int *)(d + samp_at + kSample * 8),
-                                               st, d_changed) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                    std::vector<int> sstat(kSample);
-                    std::vector<uint8_t> changed((size_t)kSample * nshares);
-                    if (hipMemcpyAsync(sstat.data(), d + samp_at + kSample * 8, 4 * kSample, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        hipMemcpyAsync(changed.data(), d_changed, changed.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        hipStreamSynchronize(st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                    bool sample_ok = true;
-                    for (int s2 : sstat) sample_ok = sample_ok && s2 == 0;
-                    std::vector<int> bad, good;
-                    for (int i = 0; i < nshares; i++) {
-                        bool b = false;
-                        for (int t = 0; t < kSample && sample_ok; t++) b = b || changed[(size_t)t * nshares + i];
-                        (b ? bad : good).push_back(i);
-                    }
-                    if (sample_ok && !bad.empty() && (int)bad.size() <= e && (int)good.size() >= k) {
-                        // expected rows: the other good shares, then the bad ones, from the first k good
-                        std::vector<int> outs(good.begin() + k, good.end());
-                        const int ncheck = (int)outs.size();
-                        outs.insert(outs.end(), bad.begin(), bad.end());
-                        int *d_rows = (int *)(d_changed + changed.size() + 16 - (changed.size() % 16));
-                        rc = reencode(c, d, slot, share_len, nums, good.data(), outs.data(), (int)outs.size(), d + exp_at, st);
-                        if (rc) break;
-                        if (hipMemcpyAsync(d_rows, outs.data(), 4 * outs.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-                            launch_flag_rows(d, slot, d_rows, ncheck, d + exp_at, slot, share_len, d + flags_at, st) != hipSuccess ||
-                            hipMemcpyAsync(flags.data(), d + flags_at, share_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                            hipStreamSynchronize(st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                        std::vector<int64_t> rest_cols;
-                        for (size_t col = 0; col < share_len; col++)
-                            if (flags[col]) rest_cols.push_back((int64_t)col);
-                        // rewrite the bad shares where the good ones agree, then BW the rest on the
-                        // received data (the sample columns are already decoded: their good
-                        // shares agree now)
-                        if (launch_put_rows(d, slot, d_rows + ncheck, (int)bad.size(), d + exp_at + slot * ncheck, slot,
-                                            share_len, d + flags_at, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                        rc = bw_columns(rest_cols);
-                        if (rc) break;
-                        done = true;
-                    }
-                }
-                if (!done) {
-                    rc = bw_columns(cols);
-                    if (rc) break;
-                }
-                for (int i = 0; i < nshares; i++)
-                    if (hipMemcpyAsync(shares[i], d + slot * i, share_len, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
-                if (rc) break;
-            }
         }
         std::vector<const uint8_t *> dptr(nshares);
-        for (int i = 0; i < nshares; i++) dptr[i] = d + slot * i;
-        rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, d + out_at, st);
+        for (int i = 0; i < nshares; i++) dptr[i] = d + L.slot * i;
+        rc = rebuild_device(c, nshares, nums, dptr.data(), (int)share_len, 1, 1, 0, 0, d + L.out_at, st);
         if (rc) break;
-        if (hipMemcpyAsync(out, d + out_at, share_len * k, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
+        if (hipMemcpyAsync(out, d + L.out_at, share_len * k, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = EC_ERR_DEVICE; break; }
         if (hipStreamSynchronize(st) != hipSuccess) rc = EC_ERR_DEVICE;
     } while (0);
     if (rc) (void)hipStreamSynchronize(st);
     release_ws(c, w);
     return rc;
+}
+
+// Syndrome rows of the sorted share set: row r = G_{k+r} G_B^-1 over the first k
+// shares (B) plus the share k+r itself, zero on every codeword.
+static int syndrome_plan(ec_ctx *c, const std::vector<int> &nums, PlanPtr *out) {
+    const int k = c->k, ns = (int)nums.size(), extra = ns - k;
+    std::vector<int> key{-3};
+    key.insert(key.end(), nums.begin(), nums.end());
+    return cached_plan(c, key, [&](std::vector<uint8_t> &M, int &rows, std::vector<int> &) {
+        std::vector<uint8_t> m((size_t)k * k);
+        for (int i = 0; i < k; i++) memcpy(&m[(size_t)i * k], &c->G[(size_t)nums[i] * k], k);
+        if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
+        rows = extra;
+        M.assign((size_t)std::max(extra, 1) * ns, 0);
+        for (int r = 0; r < extra; r++) {
+            for (int b = 0; b < k; b++) {
+                uint8_t acc = 0;
+                for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[k + r] * k + t], m[(size_t)t * k + b]);
+                M[(size_t)r * ns + b] = acc;
+            }
+            M[(size_t)r * ns + k + r] = 1;
+        }
+        return EC_OK;
+    }, out, ns);
+}
+
+int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in, uint8_t *const *pieces_in,
+                               size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
+                               uint8_t *out, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nshares > 0 && (!nums_in || !pieces_in))) return EC_ERR_INVALID_ARG;
+    const int k = c->k, ess = c->ess;
+    if (nshares < k) return EC_ERR_NOT_ENOUGH_SHARES;
+    for (int i = 0; i < nshares; i++)
+        if (nums_in[i] < 0 || nums_in[i] >= c->n) return EC_ERR_INVALID_SHARE;
+    if (k > kMaxOps || nshares > kMaxOps) return EC_ERR_UNSUPPORTED;
+    if (nstripes == 0 || nseg == 0) return EC_OK;
+    if (!out) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    // the shares in number order, as infectious sorts its []Share (the caller's arrays stay as they are)
+    std::vector<int> ord(nshares);
+    for (int i = 0; i < nshares; i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return nums_in[x] < nums_in[y]; });
+    std::vector<int> nums(nshares);
+    std::vector<uint8_t *> pcs(nshares);
+    for (int i = 0; i < nshares; i++) {
+        nums[i] = nums_in[ord[i]];
+        pcs[i] = pieces_in[ord[i]];
+    }
+    const int extra = nshares - k;
+    const size_t piece_len = nstripes * (size_t)ess;
+    bool bits = ess % 16 == 0 && aligned16(out);
+    for (auto p : pcs) bits = bits && aligned16(p);
+    Workspace *w = nullptr;
+    int rc = EC_OK;
+    uint32_t nbad = bits ? 0u : 1u;  // no bit-sliced check: take the workspace path
+    if (extra > 0 && bits) {
+        // Correct, clean case: the syndrome rows over every column, checked for zero
+        // inside the kernel (nothing stored); then Rebuild, queued behind it
+        w = acquire_ws(c, 16);
+        if (!w->d_buf) { release_ws(c, w); return EC_ERR_DEVICE; }
+        PlanPtr plan;
+        rc = syndrome_plan(c, nums, &plan);
+        if (rc) { release_ws(c, w); return rc; }
+        RsArgs a{};
+        const uint8_t *base = pcs[0];
+        for (auto p : pcs) base = std::min<const uint8_t *>(base, p);
+        a.in_base = base;
+        a.out_base = nullptr;
+        a.in_stripe_stride = ess;
+        a.out_stripe_stride = ess;
+        for (int i = 0; i < nshares; i++) {
+            a.in_off[i] = pcs[i] - base;
+            a.copy_off[i] = -1;
+        }
+        a.in_seg_stride = piece_seg_stride;
+        a.zero_check = (uint32_t *)w->d_buf;
+        std::vector<int64_t> out_off(std::max(extra, 1), 0);
+        fill_geometry(a, ess, (int64_t)nstripes, (int64_t)nseg);
+        if (hipMemsetAsync(w->d_buf, 0, 4, s) != hipSuccess) rc = EC_ERR_DEVICE;
+        if (!rc) rc = run_matmul(c, a, out_off.data(), *plan, (int64_t)nseg, true, s);
+        if (!rc && hipMemcpyAsync(&nbad, w->d_buf, 4, hipMemcpyDeviceToHost, s) != hipSuccess) rc = EC_ERR_DEVICE;
+    }
+    std::vector<const uint8_t *> cp(pcs.begin(), pcs.end());
+    if (!rc)
+        rc = rebuild_device(c, nshares, nums.data(), cp.data(), ess, (int64_t)nstripes, (int64_t)nseg,
+                            piece_seg_stride, out_seg_stride, out, s);
+    if (extra > 0 && !rc && hipStreamSynchronize(s) != hipSuccess) rc = EC_ERR_DEVICE;
+    if (w) {  // (released before the error path takes a workspace of its own)
+        if (rc) (void)hipStreamSynchronize(s);
+        release_ws(c, w);
+    }
+    if (extra > 0 && !rc) {
+        for (size_t g = 0; g < nseg && nbad != 0 && !rc; g++) {
+            // errors (or no bit-sliced check): segment by segment, Correct in a
+            // workspace, write the corrected shares back into the caller's pieces
+            // (infectious corrects share.Data in place), Rebuild again from them
+            for (int i = 0; i < nshares; i++) {
+                pcs[i] = pieces_in[ord[i]] + (int64_t)g * piece_seg_stride;
+                cp[i] = pcs[i];
+            }
+            uint8_t *gout = out + (int64_t)g * out_seg_stride;
+            const CorrectLayout L(piece_len, nshares, k, 0);
+            Workspace *cw = acquire_ws(c, L.bytes);
+            if (!cw->d_buf || !cw->stream) rc = EC_ERR_DEVICE;
+            hipStream_t st = cw->stream;
+            for (int i = 0; i < nshares && !rc; i++)
+                if (hipMemcpyAsync(cw->d_buf + L.slot * i, pcs[i], piece_len, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                    rc = EC_ERR_DEVICE;
+            bool changed = false;
+            if (!rc) rc = correct_device(c, cw->d_buf, L, piece_len, nums.data(), nshares, st, &changed);
+            for (int i = 0; i < nshares && !rc && changed; i++)
+                if (hipMemcpyAsync(pcs[i], cw->d_buf + L.slot * i, piece_len, hipMemcpyDeviceToDevice, st) != hipSuccess)
+                    rc = EC_ERR_DEVICE;
+            if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = EC_ERR_DEVICE;
+            if (cw->stream) (void)hipStreamSynchronize(st);
+            release_ws(c, cw);
+            if (!rc && changed) rc = rebuild_device(c, nshares, nums.data(), cp.data(), ess, (int64_t)nstripes, 1, 0, 0, gout, s);
+            if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EC_ERR_DEVICE;
+        }
+    }
+    return rc;
+}
+
+int ec_decode_segments(const ec_ctx *c, int nshares, const int *nums, uint8_t *const *pieces, size_t nstripes,
+                       uint8_t *out, ec_stream stream) {
+    return ec_decode_segments_batched(c, nshares, nums, pieces, nstripes, 1, 0, 0, out, stream);
 }
 
 }  // extern "C"

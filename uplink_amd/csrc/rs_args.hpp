@@ -44,6 +44,10 @@ struct RsArgs {
     int64_t blocks_per_seg;   // ceil(chunks_per_seg / 64)
     int64_t total_blocks;     // blocks_per_seg * nseg
     uint32_t *queue;          // zeroed work counter of this launch (null: static assignment)
+    // runtime-matrix kernel: when set, the computed rows are checked for zero
+    // instead of stored (syndrome rows of ec_decode_segments); each wave that
+    // finds a non-zero byte in a valid column adds 1 here
+    uint32_t *zero_check;
     int32_t ess;              // erasure share size, multiple of 16 for the bit-sliced path
     int32_t cps;              // ess / 16 (16-byte chunks per share per stripe)
     int32_t nin;              // number of inputs (k)

@@ -19,9 +19,9 @@ EncoderKernel UPLINK_AOT_NAME(UPLINK_AOT_K, UPLINK_AOT_N)() {
     EncoderKernel e;
     e.k = K;
     e.n = N;
-    e.full = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, FNC, FNL>), nullptr, (FNC + FNL) * 64,
+    e.full = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, FNC, FNL, true>), nullptr, (FNC + FNL) * 64,
               enc::wgs_per_cu(K, FNC + FNL), "rs_encode_special (library)"};
-    e.parity = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, PNC, 4>), nullptr, (PNC + 4) * 64,
+    e.parity = {reinterpret_cast<const void *>(&enc::rs_encode_special<K, N, PNC, 4, false>), nullptr, (PNC + 4) * 64,
                 enc::wgs_per_cu(K, PNC + 4), "rs_encode_special (library, parity only)"};
     return e;
 }

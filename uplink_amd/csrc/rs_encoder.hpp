@@ -12,12 +12,12 @@
 //
 // One workgroup per CU, its tiles taken from the launch's work queue
 // (take_tile); a tile is two 1-KiB column blocks half a batch apart
-// (rs_tile.hpp pair_cols), a work item one chunk of its input shares.
-// Warp-specialised around a 2-slot LDS ring: while the NC compute waves (two
-// per SIMD) multiply item i, the NL loader waves bring item i+1 into the
-// other slot raw by LDS-DMA (no registers held for the loads) and turn it
-// into bit planes in place, writing the systematic data pieces on the way.
-// One LDS-only barrier per item.  DESIGN.md §4 "Encode kernel".
+// (rs_tile.hpp pair_cols), a work item one chunk of its input shares (all
+// of them up to k = 36).  Warp-specialised around an LDS ring (2 slots):
+// while the NC compute waves (two per SIMD) multiply item i, the NL loader
+// waves bring item i+1 in raw by LDS-DMA (no registers held for the loads)
+// and turn it into bit planes in place, writing the systematic data pieces on
+// the way.  One LDS-only barrier per item.  DESIGN.md §4 "Encode kernel".
 //
 // Self-contained (no library headers): the same text is compiled into the
 // library for the configurations in rs_encoder_registry.cpp and by hiprtc for
@@ -31,8 +31,22 @@ namespace enc {
 
 using namespace dev;
 
-constexpr int kSlots = 2;      // LDS ring: item i multiplied while item i+1 arrives and is bit-sliced
-constexpr int kMaxChunk = 36;  // input shares per slot: 2 slots x 36 x 2 KiB = 144 KiB
+// LDS ring of kSlots items.  While the compute waves multiply item i, the
+// loaders bit-slice item i+1 and the LDS-DMA loads of items i+2 .. i+kAhead
+// are in flight (kAhead = kSlots - 1).  The product runs 2 slots of whole
+// tiles (all k inputs, up to 36: 2 x 58 KiB for k = 29): 3 or 4 slots need
+// items of at most 15 inputs to fit the LDS, and measured slower (RS(29,80)
+// 51.2-51.8 vs 48.5 us per segment, DESIGN.md §4 "Encode kernel").  -D
+// overrides are for A/B builds (tools/exp/build_enc_variants.sh).
+#ifndef UPLINK_ENC_SLOTS
+#define UPLINK_ENC_SLOTS 2
+#endif
+#ifndef UPLINK_ENC_MAX_CHUNK
+#define UPLINK_ENC_MAX_CHUNK 36
+#endif
+constexpr int kSlots = UPLINK_ENC_SLOTS;
+constexpr int kAhead = kSlots - 1;               // items between a load's issue and that item's multiply
+constexpr int kMaxChunk = UPLINK_ENC_MAX_CHUNK;  // input shares per item
 constexpr int chunks_of(int K) { return (K + kMaxChunk - 1) / kMaxChunk; }
 constexpr int chunk_size(int K) { return (K + chunks_of(K) - 1) / chunks_of(K); }
 
@@ -120,53 +134,74 @@ __device__ __forceinline__ void dma_1k(const uint8_t *g, uint32_t lds) {
         : "memory");
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 16].
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63] (gfx9's 6-bit counter).
 __device__ __forceinline__ void wait_vm(int n) {
     switch (n) {
 #define UPLINK_WAIT_VM(N) \
     case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-        UPLINK_WAIT_VM(1) UPLINK_WAIT_VM(2) UPLINK_WAIT_VM(3) UPLINK_WAIT_VM(4) UPLINK_WAIT_VM(5) UPLINK_WAIT_VM(6)
-        UPLINK_WAIT_VM(7) UPLINK_WAIT_VM(8) UPLINK_WAIT_VM(9) UPLINK_WAIT_VM(10) UPLINK_WAIT_VM(11) UPLINK_WAIT_VM(12)
-        UPLINK_WAIT_VM(13) UPLINK_WAIT_VM(14) UPLINK_WAIT_VM(15) UPLINK_WAIT_VM(16)
+        UPLINK_WAIT_VM(1) UPLINK_WAIT_VM(2) UPLINK_WAIT_VM(3) UPLINK_WAIT_VM(4) UPLINK_WAIT_VM(5) UPLINK_WAIT_VM(6) UPLINK_WAIT_VM(7) UPLINK_WAIT_VM(8)
+        UPLINK_WAIT_VM(9) UPLINK_WAIT_VM(10) UPLINK_WAIT_VM(11) UPLINK_WAIT_VM(12) UPLINK_WAIT_VM(13) UPLINK_WAIT_VM(14) UPLINK_WAIT_VM(15) UPLINK_WAIT_VM(16)
+        UPLINK_WAIT_VM(17) UPLINK_WAIT_VM(18) UPLINK_WAIT_VM(19) UPLINK_WAIT_VM(20) UPLINK_WAIT_VM(21) UPLINK_WAIT_VM(22) UPLINK_WAIT_VM(23) UPLINK_WAIT_VM(24)
+        UPLINK_WAIT_VM(25) UPLINK_WAIT_VM(26) UPLINK_WAIT_VM(27) UPLINK_WAIT_VM(28) UPLINK_WAIT_VM(29) UPLINK_WAIT_VM(30) UPLINK_WAIT_VM(31) UPLINK_WAIT_VM(32)
+        UPLINK_WAIT_VM(33) UPLINK_WAIT_VM(34) UPLINK_WAIT_VM(35) UPLINK_WAIT_VM(36) UPLINK_WAIT_VM(37) UPLINK_WAIT_VM(38) UPLINK_WAIT_VM(39) UPLINK_WAIT_VM(40)
+        UPLINK_WAIT_VM(41) UPLINK_WAIT_VM(42) UPLINK_WAIT_VM(43) UPLINK_WAIT_VM(44) UPLINK_WAIT_VM(45) UPLINK_WAIT_VM(46) UPLINK_WAIT_VM(47) UPLINK_WAIT_VM(48)
+        UPLINK_WAIT_VM(49) UPLINK_WAIT_VM(50) UPLINK_WAIT_VM(51) UPLINK_WAIT_VM(52) UPLINK_WAIT_VM(53) UPLINK_WAIT_VM(54) UPLINK_WAIT_VM(55) UPLINK_WAIT_VM(56)
+        UPLINK_WAIT_VM(57) UPLINK_WAIT_VM(58) UPLINK_WAIT_VM(59) UPLINK_WAIT_VM(60) UPLINK_WAIT_VM(61) UPLINK_WAIT_VM(62) UPLINK_WAIT_VM(63)
 #undef UPLINK_WAIT_VM
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
 
-template <int K, int N, int NC, int NL>
+// COPY: the full encode (the systematic data pieces written too); false: the
+// parity-only form (EC_FLAG_PARITY_ONLY), a kernel of its own name.
+template <int K, int N, int NC, int NL, bool COPY>
 __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
     constexpr int R = N - K;
     constexpr int OPW = (R + NC - 1) / NC;
     constexpr int NCH = chunks_of(K), KC = chunk_size(K);
     constexpr int PER = (KC + NL - 1) / NL;
-    static_assert(2 * PER <= 63, "a loader's DMAs of one item must fit the vmcnt counter");
+    constexpr int A = kAhead;
+    // a loader waits with at most 2(A-1) items of its DMAs and copy-through stores issued after the awaited ones
+    static_assert(4 * (A - 1) * PER <= 63 && A >= 1, "a loader's VMEM ops in flight must fit the vmcnt counter");
     constexpr int SLOT = KC * 2048;  // bytes
-    // The first K0 tiles are taken before the loop; the loop takes tile m at
-    // item m*NCH - 3 and publishes it one item later, before its first DMA at
-    // item m*NCH - 1.
-    constexpr int K0 = (3 + NCH - 1) / NCH;
+    static_assert(kSlots * SLOT <= 150 * 1024, "LDS ring too large");
+    // Tile m (items m*NCH ..) is taken by compute wave 0 at the start of item
+    // m*NCH - A - 1 and published in s_q before that item's barrier, so the
+    // loaders know it when they issue its first DMAs at item m*NCH - A.  The
+    // first K0 tiles are taken before the loop.
+    constexpr int K0 = (A + 1 + NCH - 1) / NCH;
     __shared__ __attribute__((aligned(16))) u32x4 ring[kSlots * SLOT / 16];
     __shared__ int32_t s_q[8];  // tile of the m-th take, at m & 7
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool loader = wave >= NC;
     const int lw = wave - NC;
-    const bool taker = wave == NC && lane == 0;  // takes the tiles; the others read s_q after a barrier
-    const bool do_copy = a.copy_off[0] >= 0;
+    const bool taker = wave == 0 && lane == 0;
+    constexpr bool do_copy = COPY;
     const int64_t P = pair_count(a);
     const uint32_t ring_addr = (uint32_t)(uint64_t)ring;  // LDS byte address (low bits of the generic pointer)
 
-    // loader: LDS-DMA of this wave's inputs of item (t, ch) into slot sl; returns the DMAs issued
+    // loader: its DMAs for an item of chunk ch (two per input share it owns); with
+    // do_copy its slice issues as many copy-through stores
+    auto ops_of = [&](int ch) -> int {
+        const int jn = K - ch * KC < KC ? K - ch * KC : KC;
+        return lw < jn ? 2 * ((jn - lw + NL - 1) / NL) : 0;
+    };
+#ifdef UPLINK_EC_CHECKED
+    constexpr bool kCountStores = false;  // the checked build may skip a store: count none (waits longer, never shorter)
+#else
+    constexpr bool kCountStores = true;
+#endif
+    // loader: LDS-DMA of this wave's inputs of item (t, ch) into slot sl
     auto issue = [&](int sl, int64_t t, int ch) {
         const TileCols c = pair_cols(a, t, lane);
         const int j0 = ch * KC, jn = K - j0 < KC ? K - j0 : KC;
-        int n = 0;
 #pragma unroll
         for (int i = 0; i < PER; i++) {
             const int j = lw + NL * i;
             if (j < jn) {
                 // columns past the end of the batch read column 0 of the same share (their
-                // planes are never stored)
+                // planes are never stored; their copy-through rewrites column 0 with itself)
                 const uint8_t *p = a.in_base + a.in_off[j0 + j];
                 const uint8_t *pa = p + (c.vA ? c.inA : 0), *pb = p + (c.vB ? c.inB : 0);
                 if (!in_range(a, pa, false, 1)) pa = a.chk_in_lo;
@@ -174,14 +209,15 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
                 const uint32_t d = __builtin_amdgcn_readfirstlane(ring_addr + (uint32_t)(sl * SLOT + j * 2048));
                 dma_1k(pa, d);
                 dma_1k(pb, d + 1024);
-                n += 2;
             }
         }
-        return n;
     };
     // loader: item (t, ch) in slot sl from raw bytes to bit planes, in place (each
     // lane rewrites its own 32 bytes); the systematic shares go to their data
-    // pieces on the way
+    // pieces on the way -- two stores per input on every lane, so the wave's
+    // count of VMEM ops is exact (a lane past the end of the batch holds column
+    // 0 of its share, which it stores to column 0 of that share's piece: the
+    // bytes already there)
     auto slice = [&](int sl, int64_t t, int ch) {
         const TileCols c = pair_cols(a, t, lane);
         const int j0 = ch * KC, jn = K - j0 < KC ? K - j0 : KC;
@@ -190,14 +226,14 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
         for (int i = 0; i < PER; i++) {
             const int j = lw + NL * i;
             if (j < jn) {
-                const u32x4 A = slot[j * 128 + lane], B = slot[j * 128 + 64 + lane];
-                const int64_t co = a.copy_off[j0 + j];
-                if (do_copy && co >= 0) {
-                    uint8_t *p = a.out_base + co;
-                    if (c.vA && in_range(a, p + c.outA, true, 2)) st16<true>(p + c.outA, A.x, A.y, A.z, A.w);
-                    if (c.vB && in_range(a, p + c.outB, true, 2)) st16<true>(p + c.outB, B.x, B.y, B.z, B.w);
+                const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
+                if constexpr (do_copy) {
+                    uint8_t *p = a.out_base + a.copy_off[j0 + j];
+                    uint8_t *qa = p + (c.vA ? c.outA : 0), *qb = p + (c.vB ? c.outB : 0);
+                    if (in_range(a, qa, true, 2)) st16<true>(qa, A4.x, A4.y, A4.z, A4.w);
+                    if (in_range(a, qb, true, 2)) st16<true>(qb, B4.x, B4.y, B4.z, B4.w);
                 }
-                uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+                uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
                 bitslice8(w);
                 slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
                 slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
@@ -211,58 +247,81 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
         for (int m = 0; m < K0; m++) s_q[m] = take_tile(a, m);
     lds_barrier();
     if (loader) {
+        // items 0 .. A-1 in flight, item 0 bit-sliced
+        int after = 0;
+#pragma unroll
+        for (int y = 0; y < A; y++) {
+            const int64_t t = tile_of(y);
+            if (t < P) {
+                issue(y % kSlots, t, y % NCH);
+                if (y > 0) after += ops_of(y % NCH);
+            }
+        }
         const int64_t t0 = tile_of(0);
         if (t0 < P) {
-            issue(0, t0, 0);
-            wait_vm(0);
+            wait_vm(after);
             slice(0, t0, 0);
         }
     }
     lds_barrier();
-    uint32_t acc[OPW][8];
-    int32_t pending = 0;  // the taker's last take, published one item later
-    int pend_m = -1;
-    for (int i = 0;; i++) {
-        const int64_t ti = tile_of(i);
-        if (ti >= P) break;
-        const int ch = i % NCH;
-        if (loader) {
-            if (pend_m >= 0 && taker) s_q[pend_m & 7] = pending;
+    if (loader) {
+        for (int i = 0;; i++) {
+            if (tile_of(i) >= P) break;
+            const int64_t ua = tile_of(i + A);
+            if (ua < P) issue((i + A) % kSlots, ua, (i + A) % NCH);
             const int64_t u1 = tile_of(i + 1);
-            if (u1 < P) issue((i + 1) % kSlots, u1, (i + 1) % NCH);
-            pend_m = -1;
-            int took = 0;
-            if ((i + 3) % NCH == 0 && (i + 3) / NCH >= K0) {
-                pend_m = (i + 3) / NCH;
-                if (taker) pending = take_tile(a, pend_m);
-                took = wave == NC && a.queue ? 1 : 0;  // the taker's wave has its atomic in flight too
-            }
             if (u1 < P) {
-                wait_vm(took);  // item i+1 has landed
+                // this wave's VMEM ops issued after item i+1's DMAs: the copy-through
+                // stores of items i+2-A .. i (sliced since) and the DMAs of items
+                // i+2 .. i+A; completion is in order, so waiting down to that many
+                // means item i+1 has landed
+                int after = 0;
+                if constexpr (do_copy && kCountStores)
+#pragma unroll
+                    for (int y = i + 2 - A; y <= i; y++)
+                        if (y >= 0) after += ops_of(y % NCH);
+#pragma unroll
+                for (int y = i + 2; y <= i + A; y++)
+                    if (tile_of(y) < P) after += ops_of(y % NCH);
+                wait_vm(after);
                 slice((i + 1) % kSlots, u1, (i + 1) % NCH);
             }
-        } else {
-            if (ch == 0) {
+            lds_barrier();
+        }
+        return;
+    }
+    // compute waves: per tile, the chunks in order with a barrier after each (the
+    // loaders' per-item barrier); the accumulators live across the chunks
+    uint32_t acc[OPW][8];
+    for (int m = 0;; m++) {
+        const int64_t ti = tile_of(m * NCH);
+        if (ti >= P) break;
 #pragma unroll
-                for (int o = 0; o < OPW; o++)
+        for (int o = 0; o < OPW; o++)
 #pragma unroll
-                    for (int p = 0; p < 8; p++) acc[o][p] = 0;
+            for (int p = 0; p < 8; p++) acc[o][p] = 0;
+        static_for<NCH>([&]<int C>() {
+            const int i = m * NCH + C;
+            // the tile of item i+A+1 onwards (when one starts there): its queue atomic
+            // returns during this item's multiply and is published before the barrier
+            int pend_m = -1;
+            int32_t pending = 0;
+            if (taker && (i + A + 1) % NCH == 0 && (i + A + 1) / NCH >= K0) {
+                pend_m = (i + A + 1) / NCH;
+                pending = take_tile(a, pend_m);
             }
+            constexpr int J0 = C * KC, JN = K - J0 < KC ? K - J0 : KC;
             const u32x4 *slot = ring + (i % kSlots) * (SLOT / 16);
-            static_for<NCH>([&]<int C>() {
-                if (ch == C) {
-                    constexpr int J0 = C * KC, JN = K - J0 < KC ? K - J0 : KC;
-                    static_for<NC>([&]<int W>() {
-                        if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN>(slot, lane, acc);
-                    });
-                }
+            static_for<NC>([&]<int W>() {
+                if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN>(slot, lane, acc);
             });
-            if (ch == NCH - 1) {
+            if (pend_m >= 0) s_q[pend_m & 7] = pending;
+            if constexpr (C == NCH - 1) {
                 const TileCols c = pair_cols(a, ti, lane);
                 store_rows<OPW, true>(a, 0, c, rbase_of(R, NC, wave), rows_of(R, NC, wave), acc);
             }
-        }
-        lds_barrier();
+            lds_barrier();
+        });
     }
 }
 

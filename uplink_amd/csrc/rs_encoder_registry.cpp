@@ -136,9 +136,9 @@ void load_compiler() {
         if (dlopen(so, RTLD_NOW | RTLD_GLOBAL | RTLD_NODELETE)) return;
 }
 
-std::string variant_expr(int k, int n, int nc, int nl) {
+std::string variant_expr(int k, int n, int nc, int nl, bool copy) {
     return "&uplink_ec::enc::rs_encode_special<" + std::to_string(k) + ", " + std::to_string(n) + ", " +
-           std::to_string(nc) + ", " + std::to_string(nl) + ">";
+           std::to_string(nc) + ", " + std::to_string(nl) + (copy ? ", true>" : ", false>");
 }
 
 // Compile (or read from the cache) the two variants of (k, n) for `arch`.
@@ -153,8 +153,8 @@ void compile_entry(JitEntry *e, std::string arch, int k, int n, bool read_cache)
         }
     }
     const std::string src = "#include \"rs_encoder.hpp\"\n";
-    const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n), enc::full_loader_waves(k, n)),
-                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n), 4);
+    const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n), enc::full_loader_waves(k, n), true),
+                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n), 4, false);
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++20"};
     uint64_t h = 0xcbf29ce484222325ull;
     for (int i = 0; i < kJitHeaderCount; i++) h = fnv1a(h, kJitHeaderTexts[i], strlen(kJitHeaderTexts[i]));

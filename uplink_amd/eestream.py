@@ -467,6 +467,22 @@ class SegmentCodec:
                                           flags, self._stream(stream))
         _raise(self.scheme.ctx, rc)
 
+    def decode_segments(self, nums: Iterable[int], piece_ptrs: Iterable[int], nstripes: int, out, nseg: int = 1,
+                        piece_seg_stride: int = 0, out_seg_stride: int = 0, stream=None):
+        """Decode (Correct + Rebuild) of a whole segment's pieces on the device
+        (ec_decode_segments; StripeReader with error detection, stripe.go:407-408):
+        corrected shares are written back into the pieces; returns when done."""
+        nums = list(nums)
+        ptrs = [self._addr(p) for p in piece_ptrs]
+        if len(ptrs) != len(nums):
+            raise ValueError("nums and piece pointers differ in length")
+        c_nums = (ctypes.c_int * max(len(nums), 1))(*nums)
+        c_ptrs = (ctypes.c_void_p * max(len(ptrs), 1))(*ptrs)
+        rc = self._lib.ec_decode_segments_batched(self.scheme.ctx, len(nums), c_nums, c_ptrs, nstripes, nseg,
+                                                  piece_seg_stride, out_seg_stride, self._addr(out),
+                                                  self._stream(stream))
+        _raise(self.scheme.ctx, rc)
+
     def rebuild_segments(self, nums: Iterable[int], piece_ptrs: Iterable[int], nstripes: int, out, nseg: int = 1,
                          piece_seg_stride: int = 0, out_seg_stride: int = 0, stream=None):
         nums = list(nums)
