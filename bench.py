@@ -301,7 +301,7 @@ def decode_with_detection(L, dev, sptr, reps: int = 4, nb: int = 16):
             rc = L.ec_decode_segments_batched(ctx, K + extra, nums, ptrs, nstripes, nb, N * plen, spad,
                                               back.data_ptr(), sptr)
             assert rc == 0, _native.strerror(rc)
-        for i in range(len(args)):  # plans made, outputs checked
+        for i in range(2 * len(args)):  # plans made (and their generated code: second use), outputs checked
             back.fill_(0)
             call(i)
             torch.cuda.synchronize()
@@ -319,6 +319,63 @@ def decode_with_detection(L, dev, sptr, reps: int = 4, nb: int = 16):
     res["verified"] = ok
     res["note"] = (f"clean shares, {nb} segments per call, wall clock per call (launch, check read-back and sync "
                    "included); 4 seeded share sets per count, plans warm; informational, not in value")
+    del segs, pcs, back
+    L.ec_destroy(ctx)
+    return res
+
+
+def fresh_share_sets(L, dev, sptr, nb: int = 16, launches: int = 12):
+    """Informational, outside the timed region: the rebuild when every launch
+    comes with a share set the context has not seen (a real download: each
+    segment's pieces come from whichever 29 nodes answered first, so its
+    decode plan is new) -- plan creation (inversion, generated code, module
+    load, tables) included, wall clock per launch, synchronous, after the
+    64-plan cache is full.  Against the same launches with warm plans."""
+    ctx = ctypes.c_void_p()
+    if L.ec_create(K, N, ESS, ctypes.byref(ctx)):
+        return {}
+    nstripes = (RAW_SEGMENT + 4 + K * ESS - 1) // (K * ESS)
+    spad, plen = nstripes * K * ESS, nstripes * ESS
+    segs = torch.randint(0, 256, (nb, spad), dtype=torch.uint8, device=dev)
+    pcs = torch.empty((nb, N, plen), dtype=torch.uint8, device=dev)
+    assert L.ec_encode_segments(ctx, segs.data_ptr(), nb, nstripes, pcs.data_ptr(), 0, sptr) == 0
+    back = torch.empty_like(segs)
+    rng = np.random.default_rng(64)
+
+    def subset():  # 16..29 missing data shares, as bench.py's random sets
+        return sorted(int(x) for x in rng.permutation(N)[:K])
+
+    def run(nums, n):
+        cn = (ctypes.c_int * K)(*nums)
+        cp = (ctypes.c_void_p * K)(*[pcs.data_ptr() + i * plen for i in nums])
+        assert L.ec_rebuild_segments_batched(ctx, K, cn, cp, nstripes, n, N * plen, spad, back.data_ptr(), sptr) == 0
+    for _ in range(70):  # fill the plan cache past its 64 entries
+        run(subset(), 1)
+    torch.cuda.synchronize()
+    res = {}
+    for n in (1, nb):
+        sets = [subset() for _ in range(launches)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in sets:
+            run(s, n)
+            torch.cuda.synchronize()
+        fresh = (time.perf_counter() - t0) / launches
+        t0 = time.perf_counter()
+        for s in sets:  # the same sets again: the plan's generated code is made now
+            run(s, n)
+            torch.cuda.synchronize()
+        second = (time.perf_counter() - t0) / launches
+        t0 = time.perf_counter()
+        for s in sets:  # and once more: plans and code warm
+            run(s, n)
+            torch.cuda.synchronize()
+        warm = (time.perf_counter() - t0) / launches
+        res[f"{n} segment(s) per launch"] = {"first_launch_us": round(fresh * 1e6, 1),
+                                             "second_launch_us": round(second * 1e6, 1),
+                                             "warm_launch_us": round(warm * 1e6, 1)}
+    res["note"] = ("EC_BODY_AUTO: a plan's first launch runs the jump table (no code generation or module "
+                   "load), its second makes and runs the plan's straight-line code")
     del segs, pcs, back
     L.ec_destroy(ctx)
     return res
@@ -597,6 +654,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_other_configs:
         line["other_configs"] = other_configs(L, dev, sptr)
+        line["other_configs"]["RS(29,80) rebuild, a new share set every launch"] = fresh_share_sets(L, dev, sptr)
         if hasattr(L, "ec_decode_segments_batched"):  # (an older --lib build lacks it)
             line["other_configs"]["RS(29,80) decode with error detection"] = decode_with_detection(L, dev, sptr)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

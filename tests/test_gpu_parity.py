@@ -109,10 +109,14 @@ def test_full_size_rs_29_80_64mib(oracle):
     for body in (_native.EC_BODY_AUTO, _native.EC_BODY_JUMP_TABLE):
         assert sch._lib.ec_set_body(sch._ctx, body) == 0
         for nums in (list(range(51, 80)), sorted(np.random.default_rng(29).choice(80, 29, replace=False).tolist())):
-            out = gpu_rebuild(sch, d_pieces, nums, 9040)[0]
-            assert np.array_equal(out, seg)
-            assert eestream.unpad(out.tobytes()) == raw.tobytes()
-            assert sch._lib.ec_last_body(sch._ctx) == (body or _native.EC_BODY_STRAIGHT_LINE)
+            # EC_BODY_AUTO: a plan's first launch on the jump table, its second on generated code
+            for use in range(2 if body == _native.EC_BODY_AUTO else 1):
+                out = gpu_rebuild(sch, d_pieces, nums, 9040)[0]
+                assert np.array_equal(out, seg)
+                assert eestream.unpad(out.tobytes()) == raw.tobytes()
+                want = _native.EC_BODY_JUMP_TABLE if body == _native.EC_BODY_JUMP_TABLE or use == 0 else \
+                    _native.EC_BODY_STRAIGHT_LINE
+                assert sch._lib.ec_last_body(sch._ctx) == want
 
 
 def test_full_size_rs_20_60_ess4096(oracle):
@@ -555,14 +559,18 @@ def test_straight_line_body_vs_oracle(oracle, k, n, ess, stripes):
 
 
 def test_auto_body_uses_straight_line_for_segments(oracle):
-    """EC_BODY_AUTO: a whole segment's rebuild runs the plan's generated code,
-    a per-stripe call the jump table; both bit-exact."""
+    """EC_BODY_AUTO: a whole segment's rebuild runs the plan's generated code
+    from the plan's second launch on (the first, which may be its only one,
+    runs the jump table: no code generation or module load for a share set
+    seen once), a per-stripe call the jump table; all bit-exact."""
     k, n, ess, stripes = 29, 80, 256, 600  # 75 tiles of 2048 columns (the threshold is 64)
     rng = np.random.default_rng(77)
     seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
     sch = scheme(k, n, ess)
     d_pieces = gpu_encode(sch, seg)
     nums = list(range(n - k, n))
+    assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg)
+    assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_JUMP_TABLE
     assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg)
     assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
     assert np.array_equal(gpu_rebuild(sch, d_pieces[:, :, :ess].contiguous(), nums, 1)[0], seg[:k * ess])
@@ -649,6 +657,7 @@ def test_straight_line_plans_evicted_and_shared_across_threads(oracle):
     against the segment."""
     k, n, ess, stripes = 4, 10, 256, 512  # 64 tiles per segment
     sch = scheme(k, n, ess)
+    assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0  # generated code from the first launch
     rng = np.random.default_rng(91)
     seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
     d_pieces = gpu_encode(sch, seg)
@@ -894,3 +903,22 @@ def test_decode_segments_batched(oracle):
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), segs)
         assert np.array_equal(d_pieces.cpu().numpy(), refs)  # the bad piece corrected in place
+
+
+def test_auto_body_fresh_share_sets_recycle_plan_memory(oracle):
+    """EC_BODY_AUTO with a new share set per call, past the 64 cached plans:
+    each set's first launch on the jump table, its second on generated code;
+    evicted plans return their tables to the context's arena, and the
+    recycled memory serves the next plans (every result checked)."""
+    k, n, ess, stripes = 5, 12, 256, 512
+    sch = scheme(k, n, ess)
+    rng = np.random.default_rng(92)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    d_pieces = gpu_encode(sch, seg)
+    import itertools
+    sets = [list(c) for c in itertools.combinations(range(n), k) if any(x >= k for x in c)]
+    rng.shuffle(sets)
+    for nums in sets[:150]:
+        for want in (_native.EC_BODY_JUMP_TABLE, _native.EC_BODY_STRAIGHT_LINE):
+            assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), nums
+            assert sch._lib.ec_last_body(sch._ctx) == want

@@ -15,6 +15,7 @@
 #include <list>
 #include <memory>
 #include <deque>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -39,7 +40,65 @@ namespace {
 // Plans of at most kMaxOps rows can also carry the matrix as straight-line
 // code (rs_sl.hpp): a module made from the template code object on the first
 // launch that wants it, and the absolute addresses of its segments.
+// Device memory for the plans' small tables (coefficients, leaf addresses,
+// segment addresses), carved from 2-MiB chunks in power-of-two classes and
+// recycled, so that making or evicting a plan costs no hipMalloc / hipFree
+// (a fresh share set per segment is the download path's common case).  The
+// chunks go back to HIP when the context and every plan are gone.
+struct DevArena {
+    static constexpr size_t kChunk = 2u << 20, kMinClass = 256;
+    std::mutex mu;
+    std::vector<void *> chunks;
+    uint8_t *cur = nullptr;
+    size_t left = 0;
+    std::vector<std::vector<uint8_t *>> free_by_class = std::vector<std::vector<uint8_t *>>(32);
+    static int cls(size_t n) {
+        int c = 0;
+        while ((kMinClass << c) < n) c++;
+        return c;
+    }
+    uint8_t *alloc(size_t n) {
+        const int c = cls(n);
+        const size_t sz = kMinClass << c;
+        std::lock_guard<std::mutex> g(mu);
+        if (!free_by_class[c].empty()) {
+            uint8_t *p = free_by_class[c].back();
+            free_by_class[c].pop_back();
+            return p;
+        }
+        if (sz > kChunk) {  // (no plan table is this large; served directly)
+            void *p = nullptr;
+            if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
+            chunks.push_back(p);
+            return (uint8_t *)p;
+        }
+        if (left < sz) {
+            void *p = nullptr;
+            if (hipMalloc(&p, kChunk) != hipSuccess) return nullptr;
+            chunks.push_back(p);
+            cur = (uint8_t *)p;
+            left = kChunk;
+        }
+        uint8_t *p = cur;
+        cur += sz;
+        left -= sz;
+        return p;
+    }
+    void release(uint8_t *p, size_t n) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        free_by_class[cls(n)].push_back(p);
+    }
+    ~DevArena() {
+        for (void *p : chunks) (void)hipFree(p);
+    }
+};
+
 struct MatPlan {
+    std::shared_ptr<DevArena> arena;  // where d_coef, d_tgt and d_sl live
+    size_t coef_bytes = 0, sl_bytes = 0;
+    std::vector<size_t> tgt_bytes;
+    std::atomic<int> launches{0};     // launches made with this plan (straight-line code from the second on)
     std::vector<int> key;          // what the matrix is (decode: chosen share ids; see plan keys below)
     std::vector<int> missing;      // decode plans: the data positions rebuilt, in row order
     int rows = 0, nin = 0, coef_ld = 0;
@@ -81,10 +140,11 @@ struct MatPlan {
     }
     ~MatPlan() {
         for (auto &u : uses) (void)hipEventSynchronize(u.second), (void)hipEventDestroy(u.second);
-        if (d_coef) (void)hipFree(d_coef);
-        for (uint64_t *t : d_tgt)
-            if (t) (void)hipFree(t);
-        if (d_sl) (void)hipFree(d_sl);
+        if (arena) {
+            arena->release(d_coef, coef_bytes);
+            for (size_t i = 0; i < d_tgt.size(); i++) arena->release((uint8_t *)d_tgt[i], tgt_bytes[i]);
+            arena->release((uint8_t *)d_sl, sl_bytes);
+        }
         if (sl_mod) (void)hipModuleUnload(sl_mod);
     }
 };
@@ -161,6 +221,7 @@ struct ec_ctx {
     HostPipe pipe;
     std::vector<uint8_t> G;        // n x k
     hipStream_t setup = nullptr;   // plan uploads (synchronous, never a caller's stream)
+    std::shared_ptr<DevArena> arena = std::make_shared<DevArena>();
     std::mutex setup_mu;
     std::mutex mu;
     std::list<PlanPtr> plans;      // decode / re-encode plans, MRU first
@@ -306,6 +367,7 @@ void set_extents(RsArgs &a, int64_t nseg, uint32_t *chk) {
 // Upload M (rows x nin, row-major) and its leaf-address tables; synchronous.
 int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int nin, PlanPtr *out) {
     PlanPtr p = std::make_shared<MatPlan>();
+    p->arena = c->arena;
     p->key = std::move(key);
     p->rows = rows;
     p->nin = nin;
@@ -315,7 +377,9 @@ int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int 
     for (int r = 0; r < rows; r++)
         for (int j = 0; j < nin; j++) coef[(size_t)j * p->coef_ld + r] = M[(size_t)r * nin + j];
     std::lock_guard<std::mutex> g(c->setup_mu);
-    HIP_TRY(hipMalloc(&p->d_coef, coef.size()));
+    p->coef_bytes = coef.size();
+    p->d_coef = p->arena->alloc(coef.size());
+    if (!p->d_coef) return hip_fail(hipErrorOutOfMemory);
     HIP_TRY(hipMemcpyAsync(p->d_coef, coef.data(), coef.size(), hipMemcpyHostToDevice, c->setup));
     for (int r0 = 0; r0 < std::max(rows, 1); r0 += kMaxOps) {
         RsArgs t{};
@@ -323,9 +387,10 @@ int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int 
         t.coef_ld = p->coef_ld;
         t.nin = nin;
         t.nout = std::min(kMaxOps, rows - r0);
-        uint64_t *tgt = nullptr;
-        HIP_TRY(hipMalloc(&tgt, jt_targets_bytes(t)));
+        uint64_t *tgt = (uint64_t *)p->arena->alloc(jt_targets_bytes(t));
+        if (!tgt) return hip_fail(hipErrorOutOfMemory);
         p->d_tgt.push_back(tgt);
+        p->tgt_bytes.push_back(jt_targets_bytes(t));
         HIP_TRY(launch_jt_targets(t, tgt, c->setup));
     }
     HIP_TRY(hipStreamSynchronize(c->setup));  // `coef` (pageable) is consumed before it goes away
@@ -499,14 +564,15 @@ void ensure_sl(ec_ctx *c, MatPlan &plan) {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
     uint64_t *d = nullptr;
+    const size_t dbytes = (offs.size() + 1) * sizeof(uint64_t);
     auto fail = [&](hipError_t e) {
         hip_fail(e);
-        if (d) (void)hipFree(d);
+        if (d) plan.arena->release((uint8_t *)d, dbytes);
         if (mod) (void)hipModuleUnload(mod);
     };
     hipError_t e = hipModuleLoadData(&mod, img.data());
     if (e == hipSuccess) e = hipModuleGetFunction(&fn, mod, "rs_sl_where");
-    if (e == hipSuccess) e = hipMalloc(&d, (offs.size() + 1) * sizeof(uint64_t));
+    if (e == hipSuccess && !(d = (uint64_t *)plan.arena->alloc(dbytes))) e = hipErrorOutOfMemory;
     if (e != hipSuccess) return fail(e);
     void *args[] = {&d};
     uint64_t base = 0;
@@ -521,6 +587,7 @@ void ensure_sl(ec_ctx *c, MatPlan &plan) {
     if (e != hipSuccess) return fail(e);
     plan.sl_mod = mod;
     plan.d_sl = d;
+    plan.sl_bytes = dbytes;
 }
 
 // Launch the product described by `a` with the rows of `plan` (out_off gives
@@ -541,8 +608,13 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64
         if (done > 0)
             for (int j = 0; j < a.nin; j++) a.copy_off[j] = -1;
         set_extents(a, nseg, c->d_chk);
+        // EC_BODY_AUTO: a plan's first launch runs the jump table, the straight-line
+        // code is made for its second (a share set seen once -- a download's
+        // segment, most often -- never pays the code generation and module load,
+        // ~0.9 ms against ~50 us of kernel time per segment)
         const bool want_sl = bitsliced && total_rows <= kMaxOps && c->body != EC_BODY_JUMP_TABLE &&
-                             (c->body == EC_BODY_STRAIGHT_LINE || a.total_tiles >= kSlMinTiles);
+                             (c->body == EC_BODY_STRAIGHT_LINE ||
+                              (a.total_tiles >= kSlMinTiles && plan.launches.load() > 0));
         if (want_sl) ensure_sl(c, plan);
         if (want_sl && plan.d_sl) {
             a.jt_tgt = plan.d_sl;
@@ -558,6 +630,7 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64
             a.total_tiles = keep;
         }
         plan.note_use(s);
+        plan.launches++;
         if (int rc = after_launch(c->d_chk, s)) return rc;
         done += rows;
         blk++;
