@@ -223,13 +223,36 @@ __global__ __launch_bounds__(NW * 64) void enc_queue(const uint8_t *in, uint8_t 
     }
 }
 
+// PROBE_RAND=1: buffers filled with pseudo-random bytes instead of a constant
+// (the product's inputs are random; the round-3 logs before this option ran
+// on memset data)
+__global__ void fill_rand(uint8_t *p, int64_t n16, uint32_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t x = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+        uint32_t w[4];
+        for (int k = 0; k < 4; k++) {
+            x ^= x >> 30, x *= 0xBF58476D1CE4E5B9ull, x ^= x >> 27, x *= 0x94D049BB133111EBull, x ^= x >> 31;
+            w[k] = (uint32_t)x;
+        }
+        *(uint4 *)(p + i * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+static bool g_rand = false;
+static void fill(uint8_t *p, int64_t bytes, int c, uint32_t seed) {
+    if (g_rand) hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, p, bytes / 16, seed);
+    else (void)hipMemset(p, c, bytes);
+    (void)hipDeviceSynchronize();
+}
+
 int main(int argc, char **argv) {
+    g_rand = getenv("PROBE_RAND") && atoi(getenv("PROBE_RAND")) != 0;
+    printf("data: %s\n", g_rand ? "pseudo-random" : "constant (memset)");
     uint8_t *in, *out;
     CK(hipMalloc(&in, SPAD * NSEG));
     const int64_t OUTB = (int64_t)N * PLEN * NSEG;
     CK(hipMalloc(&out, OUTB));
-    CK(hipMemset(in, 0x5a, SPAD * NSEG));
-    CK(hipMemset(out, 0x33, OUTB));
+    fill(in, SPAD * NSEG, 0x5a, 1);
+    fill(out, OUTB, 0x33, 2);
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     hipEvent_t e0, e1;
@@ -326,8 +349,8 @@ int main(int argc, char **argv) {
             CK(hipMalloc(&ins[a], SPAD * NSEG + (a << 21)));
             CK(hipMalloc(&outs[a], OUTB + (a << 21)));
             ins[a] += (a << 21), outs[a] += (a << 21);  // a different 2-MiB phase, too
-            CK(hipMemset(ins[a], 0x5a, SPAD * NSEG));
-            CK(hipMemset(outs[a], 0x33, OUTB));
+            fill(ins[a], SPAD * NSEG, 0x5a, 3 + a);
+            fill(outs[a], OUTB, 0x33, 7 + a);
         }
         const int64_t nt2 = (int64_t)NSEG * (CPS / 128), nt1 = (int64_t)NSEG * (CPS / 64);
         struct Var {

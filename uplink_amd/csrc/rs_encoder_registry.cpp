@@ -154,7 +154,7 @@ void compile_entry(JitEntry *e, std::string arch, int k, int n, bool read_cache)
     }
     const std::string src = "#include \"rs_encoder.hpp\"\n";
     const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n), enc::full_loader_waves(k, n), true),
-                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n), 4, false);
+                      parity = variant_expr(k, n, enc::parity_compute_waves(k, n), enc::loader_waves(k, n), false);
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-std=c++20"};
     uint64_t h = 0xcbf29ce484222325ull;
     for (int i = 0; i < kJitHeaderCount; i++) h = fnv1a(h, kJitHeaderTexts[i], strlen(kJitHeaderTexts[i]));
@@ -315,7 +315,8 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
     const int pnc = enc::parity_compute_waves(k, n), fnc = enc::full_compute_waves(k, n),
               fnl = enc::full_loader_waves(k, n);
     ek->full = {nullptr, f_full, (fnc + fnl) * 64, enc::wgs_per_cu(k, fnc + fnl), "rs_encode_special (jit)"};
-    ek->parity = {nullptr, f_par, (pnc + 4) * 64, enc::wgs_per_cu(k, pnc + 4), "rs_encode_special (jit, parity only)"};
+    const int pnl = enc::loader_waves(k, n);
+    ek->parity = {nullptr, f_par, (pnc + pnl) * 64, enc::wgs_per_cu(k, pnc + pnl), "rs_encode_special (jit, parity only)"};
     EncoderKernel *out = ek.get();
     e->loaded[dev] = std::move(ek);
     return out;

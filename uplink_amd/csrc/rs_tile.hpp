@@ -98,6 +98,21 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 // s_waitcnt vmcnt(0)), does not drain outstanding global stores.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// One 1-KiB LDS-DMA: 16 bytes per lane from g (per lane) to the LDS byte
+// address lds (wave-uniform) + 16 lane, non-temporal.  Inline asm, so the
+// compiler neither waits for it nor moves memory operations across it: the
+// kernel's counted vmcnt waits retire it.  (M0 written by SALU and read by an
+// LDS-DMA right after needs a wait state: the s_nop.)
+// M0 is the compiler's, so the asm puts it back.
+__device__ __forceinline__ void dma_1k(const uint8_t *g, uint32_t lds) {
+    uint32_t save;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(save)
+        : "v"(g), "s"(lds)
+        : "memory");
+}
+
 // Checked build (UPLINK_EC_CHECKED, tests/test_c_abi.py): every 16-byte
 // global access of the stripe kernels is compared with the launch's declared
 // byte ranges; one outside them is skipped and its site recorded in
