@@ -111,84 +111,6 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
     });
 }
 
-// Row O of a finished tile (its accumulators `row`) to its parity piece at
-// the tile's columns pc.  Every lane stores both chunks: a column past the
-// end of the batch holds the parity of column 0 (its inputs were read from
-// column 0), which it writes to column 0 -- the bytes already there -- so a
-// wave's count of VMEM operations is exact.
-__device__ __forceinline__ void store_row(const RsArgs &a, const TileCols &pc, int r, const uint32_t (&row)[8]) {
-    uint32_t w[8];
-#pragma unroll
-    for (int p = 0; p < 8; p++) w[p] = row[p];
-    unbitslice8(w);
-    uint8_t *q = a.out_base + a.out_off[r];
-    uint8_t *qa = q + (pc.vA ? pc.outA : 0), *qb = q + (pc.vB ? pc.outB : 0);
-    if (in_range(a, qa, true, 3)) st16<true>(qa, w[0], w[1], w[2], w[3]);
-    if (in_range(a, qb, true, 3)) st16<true>(qb, w[4], w[5], w[6], w[7]);
-}
-
-// compute_chunk over all K inputs of a tile, with the previous tile's rows
-// (`prev`) stored on the way: row O after input 4 O + 2 (or after
-// the last input when there are too few), so a wave's
-// parity stores leave one or two at a time across the multiply instead of in
-// one burst at its end.
-template <int K, int N, int NC, int OPW, int W>
-__device__ __forceinline__ void compute_deferred(const u32x4 *slot, int lane, uint32_t (&acc)[OPW][8],
-                                                 const uint32_t (&prev)[OPW][8], const RsArgs &a,
-                                                 const TileCols &pc) {
-    constexpr int R = N - K, RB = rbase_of(R, NC, W), RN = rows_of(R, NC, W);
-    uint32_t opq = 0;
-    asm volatile("" : "+s"(opq));
-    slot += opq;
-    u32x4 nlo = slot[lane], nhi = slot[64 + lane];
-    static_for<K>([&]<int J>() {
-        const u32x4 lo4 = nlo, hi4 = nhi;
-        if constexpr (J + 1 < K) {
-            nlo = slot[(J + 1) * 128 + lane];
-            nhi = slot[(J + 1) * 128 + 64 + lane];
-        }
-        asm volatile("" ::: "memory");
-        const uint32_t x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-        uint32_t lo[16], hi[16];
-        lo[0] = 0;
-        hi[0] = 0;
-        static_for<15>([&]<int M1>() {
-            constexpr int M = M1 + 1;
-            constexpr int low = M & (-M);
-            constexpr int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
-            if constexpr (M == low) {
-                lo[M] = x[bit];
-                hi[M] = x[4 + bit];
-            } else {
-                lo[M] = lo[M ^ low] ^ x[bit];
-                hi[M] = hi[M ^ low] ^ x[4 + bit];
-            }
-        });
-        static_for<OPW>([&]<int O>() {
-            if constexpr (O < RN) {
-                constexpr uint8_t cval = gen_entry(K, K + RB + O, J);
-                static_for<8>([&]<int P>() {
-                    constexpr uint8_t row = mul_bitrow(cval, P);
-                    constexpr int L = row & 15, H = row >> 4;
-                    if constexpr (L != 0 && H != 0)
-                        acc[O][P] = __builtin_amdgcn_bitop3_b32(acc[O][P], lo[L], hi[H], 0x96);
-                    else if constexpr (L != 0)
-                        acc[O][P] ^= lo[L];
-                    else if constexpr (H != 0)
-                        acc[O][P] ^= hi[H];
-                });
-            }
-        });
-        if constexpr (J % 4 == 2 && J / 4 < RN) {
-            store_row(a, pc, RB + J / 4, prev[J / 4]);
-        }
-    });
-    // rows that found no input slot (fewer than 4 inputs per row)
-    static_for<OPW>([&]<int O>() {
-        if constexpr (O < RN && 4 * O + 2 >= K) store_row(a, pc, RB + O, prev[O]);
-    });
-}
-
 // Tile for the m-th take of this workgroup: from the launch's work queue
 // (a.queue, zeroed before the launch) or, without one, statically.  Only one
 // lane calls it; a returning vector atomic, not a scalar one.
@@ -215,123 +137,6 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
-// The fused form (no loader waves; NL = 0 below): every wave brings in its
-// share of the next tile by LDS-DMA, multiplies the current one -- storing the
-// previous tile's parity rows on the way (compute_deferred) -- then waits for
-// its DMAs, bit-slices them in place (the systematic pieces written on the
-// way) and meets the others at the tile's one barrier.  Two waves per SIMD
-// with 256 VGPRs each: room for the previous tile's accumulators.  Whole
-// tiles only (k <= kMaxChunk).
-template <int K, int N, int NC, bool COPY>
-__device__ __forceinline__ void fused_body(const RsArgs &a, u32x4 *ring, int32_t *s_q) {
-    constexpr int R = N - K, OPW = (R + NC - 1) / NC, SLOT = K * 2048;
-    constexpr int PERW = (K + NC - 1) / NC;
-    static_assert(chunks_of(K) == 1, "the fused encoder takes whole tiles");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool taker = wave == 0 && lane == 0;
-    const int64_t P = pair_count(a);
-    const uint32_t ring_addr = (uint32_t)(uint64_t)ring;
-#ifdef UPLINK_EC_CHECKED
-    constexpr bool kCountStores = false;
-#else
-    constexpr bool kCountStores = true;
-#endif
-    auto issue = [&](int sl, int64_t t) {
-        const TileCols c = pair_cols(a, t, lane);
-#pragma unroll
-        for (int i = 0; i < PERW; i++) {
-            const int j = wave + NC * i;
-            if (j < K) {
-                const uint8_t *p = a.in_base + a.in_off[j];
-                const uint8_t *pa = p + (c.vA ? c.inA : 0), *pb = p + (c.vB ? c.inB : 0);
-                if (!in_range(a, pa, false, 1)) pa = a.chk_in_lo;
-                if (!in_range(a, pb, false, 1)) pb = a.chk_in_lo;
-                const uint32_t d = __builtin_amdgcn_readfirstlane(ring_addr + (uint32_t)(sl * SLOT + j * 2048));
-                dma_1k(pa, d);
-                dma_1k(pb, d + 1024);
-            }
-        }
-    };
-    auto slice = [&](int sl, int64_t t) {
-        const TileCols c = pair_cols(a, t, lane);
-        u32x4 *slot = ring + sl * (SLOT / 16);
-#pragma unroll
-        for (int i = 0; i < PERW; i++) {
-            const int j = wave + NC * i;
-            if (j < K) {
-                const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
-                if constexpr (COPY) {
-                    uint8_t *p = a.out_base + a.copy_off[j];
-                    uint8_t *qa = p + (c.vA ? c.outA : 0), *qb = p + (c.vB ? c.outB : 0);
-                    if (in_range(a, qa, true, 2)) st16<true>(qa, A4.x, A4.y, A4.z, A4.w);
-                    if (in_range(a, qb, true, 2)) st16<true>(qb, B4.x, B4.y, B4.z, B4.w);
-                }
-                uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
-                bitslice8(w);
-                slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
-                slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
-            }
-        }
-    };
-    if (taker) {
-        s_q[0] = take_tile(a, 0);
-        s_q[1] = take_tile(a, 1);
-    }
-    lds_barrier();
-    const int64_t t0 = s_q[0];
-    if (t0 >= P) return;  // the same for every wave
-    issue(0, t0);
-    wait_vm(0);
-    slice(0, t0);
-    lds_barrier();
-    uint32_t acc[OPW][8], prev[OPW][8];
-    // one iteration of the loop: tile s_q[m & 7] from slot m & 1; the first one
-    // (no previous tile to store) is peeled, so the stores in the multiply are
-    // unconditional (a wave-uniform branch around each of them made the
-    // compiler spill 340 VGPRs)
-    auto step = [&]<bool FIRST>(int m) __attribute__((always_inline)) {
-        const int64_t tn = s_q[(m + 1) & 7];
-        int32_t pending = 0;
-        if (taker) pending = take_tile(a, m + 2);
-        if (tn < P) issue((m + 1) & 1, tn);
-#pragma unroll
-        for (int o = 0; o < OPW; o++)
-#pragma unroll
-            for (int p = 0; p < 8; p++) acc[o][p] = 0;
-        const u32x4 *slot = ring + (m & 1) * (SLOT / 16);
-        if constexpr (FIRST) {
-            static_for<NC>([&]<int W>() {
-                if (wave == W) compute_chunk<K, N, NC, OPW, W, 0, K>(slot, lane, acc);
-            });
-        } else {
-            const TileCols pc = pair_cols(a, s_q[(m - 1) & 7], lane);
-            static_for<NC>([&]<int W>() {
-                if (wave == W) compute_deferred<K, N, NC, OPW, W>(slot, lane, acc, prev, a, pc);
-            });
-        }
-        if (taker) s_q[(m + 2) & 7] = pending;
-        if (tn < P) {
-            // this wave's VMEM ops after the DMAs: the deferred parity stores
-            wait_vm(kCountStores && !FIRST ? 2 * rows_of(R, NC, wave) : 0);
-            slice((m + 1) & 1, tn);
-        }
-#pragma unroll
-        for (int o = 0; o < OPW; o++)
-#pragma unroll
-            for (int p = 0; p < 8; p++) prev[o][p] = acc[o][p];
-        lds_barrier();
-    };
-    step.template operator()<true>(0);
-    int m = 1;
-    for (; s_q[m & 7] < P; m++) step.template operator()<false>(m);
-    const TileCols pc = pair_cols(a, s_q[(m - 1) & 7], lane);
-    const int rb = rbase_of(R, NC, wave), rn = rows_of(R, NC, wave);
-    static_for<OPW>([&]<int O>() {
-        if (O < rn) store_row(a, pc, rb + O, prev[O]);
-    });
-}
-
 // COPY: the full encode (the systematic data pieces written too); false: the
 // parity-only form (EC_FLAG_PARITY_ONLY), a kernel of its own name.
 template <int K, int N, int NC, int NL, bool COPY>
@@ -339,8 +144,7 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
     constexpr int R = N - K;
     constexpr int OPW = (R + NC - 1) / NC;
     constexpr int NCH = chunks_of(K), KC = chunk_size(K);
-    constexpr int NLd = NL > 0 ? NL : 1;  // NL = 0: the fused form (fused_body)
-    constexpr int PER = (KC + NLd - 1) / NLd;
+    constexpr int PER = (KC + NL - 1) / NL;
     constexpr int A = kAhead;
     // a loader waits with at most 2(A-1) items of its DMAs and copy-through stores issued after the awaited ones
     static_assert(4 * (A - 1) * PER <= 63 && A >= 1, "a loader's VMEM ops in flight must fit the vmcnt counter");
@@ -357,26 +161,16 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool loader = wave >= NC;
     const int lw = wave - NC;
-#ifdef UPLINK_ENC_PRIO_L
-    if (loader) __builtin_amdgcn_s_setprio(UPLINK_ENC_PRIO_L);
-#endif
-#ifdef UPLINK_ENC_PRIO_C
-    if (!loader) __builtin_amdgcn_s_setprio(UPLINK_ENC_PRIO_C);
-#endif
     const bool taker = wave == 0 && lane == 0;
     constexpr bool do_copy = COPY;
     const int64_t P = pair_count(a);
     const uint32_t ring_addr = (uint32_t)(uint64_t)ring;  // LDS byte address (low bits of the generic pointer)
-    if constexpr (NL == 0) {
-        fused_body<K, N, NC, COPY>(a, ring, s_q);
-        return;
-    }
 
     // loader: its DMAs for an item of chunk ch (two per input share it owns); with
     // do_copy its slice issues as many copy-through stores
     auto ops_of = [&](int ch) -> int {
         const int jn = K - ch * KC < KC ? K - ch * KC : KC;
-        return lw < jn ? 2 * ((jn - lw + NLd - 1) / NLd) : 0;
+        return lw < jn ? 2 * ((jn - lw + NL - 1) / NL) : 0;
     };
 #ifdef UPLINK_EC_CHECKED
     constexpr bool kCountStores = false;  // the checked build may skip a store: count none (waits longer, never shorter)
@@ -524,14 +318,13 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // every other cycle); the 4-plane combinations each compute wave rebuilds per
 // input cost 14 % more VALU than with 4.
 constexpr int compute_waves(int k, int n) { return n - k >= 16 ? 8 : 4; }
-#ifndef UPLINK_ENC_FUSED
-#define UPLINK_ENC_FUSED 0
-#endif
-constexpr int loader_waves(int k, int n) {
-    return UPLINK_ENC_FUSED && chunks_of(k) == 1 && compute_waves(k, n) == 8 ? 0 : 4;
-}
+constexpr int loader_waves(int k, int n) { return 4; }
 constexpr int parity_compute_waves(int k, int n) { return compute_waves(k, n); }
-constexpr int full_compute_waves(int k, int n) { return compute_waves(k, n); }
+// The full encode with at most 40 parity rows keeps 4 compute waves: its
+// loaders' copy-through share of a tile is large enough that the 4 extra
+// waves' combinations cost more than their issue rate gains (RS(20,60) 47.2
+// vs 49.8 us per segment; RS(29,80) 50.0 vs 47.8 the other way).
+constexpr int full_compute_waves(int k, int n) { return n - k <= 40 ? 4 : compute_waves(k, n); }
 constexpr int full_loader_waves(int k, int n) { return loader_waves(k, n); }
 // One workgroup per CU: its ring takes up to 144 KiB of LDS.
 constexpr int wgs_per_cu(int k, int waves) { return 1; }

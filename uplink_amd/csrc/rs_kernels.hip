@@ -142,92 +142,6 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     }
 }
 
-// Straight-line body with the whole tile resident in LDS (whole segments,
-// k <= kDmaMaxIn): every input share of the tile arrives raw by LDS-DMA at
-// once (no staging registers, all of a wave's loads in flight together), each
-// wave bit-slices the inputs it brought in place -- copying the present data
-// shares through on the way -- and, after the tile's one barrier, the plan's
-// code segments run over the chunks back to back, reading them where they
-// lie.  The chunked kernel above waits for its loads once per chunk of 2 NW
-// inputs (8 round trips and 8 barriers per tile for m <= 16); here there is
-// one.  One workgroup per tile; 2 per CU at k = 29 (58 KiB of LDS each).
-constexpr int kDmaMaxIn = 32;  // 64 KiB of LDS: the default dynamic LDS limit
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
-    constexpr int OPW = kJtRows;
-    const int nchunks = (a.nin + 2 * NW - 1) / (2 * NW);
-    const int CH = (a.nin + nchunks - 1) / nchunks;
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    u32x4 *lds = (u32x4 *)smem;  // [nin][2 KiB]: raw bytes, then planes (the wide layout)
-    const uint32_t lds_base = (uint32_t)(uintptr_t)smem;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
-    const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
-    const int64_t tile = blockIdx.x;
-    const int64_t seg = tile / a.tiles_per_seg;
-    const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
-    const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
-    // columns past the end of the segment read column 0 of the same share
-    // (their planes are never stored, nor their bytes copied)
-    const int64_t oA = c.vA ? c.inA : 0, oB = c.vB ? c.inB : 0;
-    for (int j = wave; j < a.nin; j += NW) {
-        const uint8_t *p = in_seg + a.in_off[j];
-        const uint8_t *pa = p + oA, *pb = p + oB;
-        if (!in_range(a, pa, false, 4)) pa = a.chk_in_lo;
-        if (!in_range(a, pb, false, 4)) pb = a.chk_in_lo;
-        const uint32_t d = lds_base + (uint32_t)j * 2048;
-        dma_1k(pa, d);
-        dma_1k(pb, d + 1024);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
-    for (int j = wave; j < a.nin; j += NW) {
-        const u32x4 A4 = lds[j * 128 + lane], B4 = lds[j * 128 + 64 + lane];
-        const int64_t co = a.copy_off[j];
-        if (co >= 0) {
-            uint8_t *p = out_seg + co;
-            if (c.vA && in_range(a, p + c.outA, true, 5)) st16<true>(p + c.outA, A4.x, A4.y, A4.z, A4.w);
-            if (c.vB && in_range(a, p + c.outB, true, 5)) st16<true>(p + c.outB, B4.x, B4.y, B4.z, B4.w);
-        }
-        uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
-        bitslice8(w);
-        lds[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
-        lds[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
-    }
-    lds_barrier();
-    for (int pass = 0; pass < npass; pass++) {
-        const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
-        const int rbase = p0 + group * prow / NW;
-        const int cnt = p0 + (group + 1) * prow / NW - rbase;
-        if (cnt <= 0) continue;
-        u32x8 acc[OPW];
-#pragma unroll
-        for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
-        for (int ch = 0; ch < nchunks; ch++)
-            sl_segment(acc, lds_base + (uint32_t)lane * 16 + (uint32_t)(ch * CH) * 2048,
-                       a.jt_tgt + (pass * nchunks + ch) * NW + group);
-        uint32_t rows[OPW][8];
-#pragma unroll
-        for (int o = 0; o < OPW; o++)
-#pragma unroll
-            for (int p = 0; p < 8; p++) rows[o][p] = acc[o][p];
-        if (a.zero_check) {
-            uint32_t any = 0;
-#pragma unroll
-            for (int o = 0; o < OPW; o++)
-                if (o < cnt)
-#pragma unroll
-                    for (int p = 0; p < 8; p++) any |= rows[o][p];
-            any &= (c.vA ? 0x0F0F0F0Fu : 0u) | (c.vB ? 0xF0F0F0F0u : 0u);
-            if (__ballot(any != 0) != 0 && lane == 0) atomicAdd(a.zero_check, 1u);
-        } else {
-            store_rows<OPW, true>(a, seg, c, rbase, cnt, rows);
-        }
-    }
-}
-
 template <int NW>
 size_t jt_lds_bytes(const RsArgs &) {
     return (size_t)2 * 2 * NW * 8 * 64 * 4;
@@ -356,21 +270,6 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     // per segment).  The encoder keeps its persistent grid (one
     // workgroup per tile: 809 -> 1248 us).
     if (grid <= 0) grid = (int)std::min<int64_t>(std::max<int64_t>(a.total_tiles, 1), 1 << 30);
-#ifndef UPLINK_REB_DMA
-#define UPLINK_REB_DMA 0
-#endif
-    if (SL && UPLINK_REB_DMA && a.nin <= kDmaMaxIn) {
-        const size_t lds = (size_t)a.nin * 2048;
-        switch (sl::split_for(a.nout).nw) {
-#define UPLINK_DMA_CASE(W) \
-    case W: hipLaunchKernelGGL((rs_matmul_dma<W>), dim3(grid), dim3(W * 64), lds, s, a); break;
-            UPLINK_DMA_CASE(2) UPLINK_DMA_CASE(3) UPLINK_DMA_CASE(5) UPLINK_DMA_CASE(6) UPLINK_DMA_CASE(7)
-            UPLINK_DMA_CASE(8)
-#undef UPLINK_DMA_CASE
-            default: hipLaunchKernelGGL((rs_matmul_dma<4>), dim3(grid), dim3(4 * 64), lds, s, a);
-        }
-        return hipGetLastError();
-    }
     switch (SL ? sl::split_for(a.nout).nw : jt_waves(a.nout)) {
     case 8:
         hipLaunchKernelGGL((rs_matmul_jt<8, true>), dim3(grid), dim3(8 * 64), jt_lds_bytes<8>(a), s, a);
