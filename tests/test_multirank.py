@@ -100,3 +100,32 @@ def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
     assert line["ranks_seen"] == 2
     assert len(line["rank_wall_s"]) == 2 and all(w > 0 for w in line["rank_wall_s"])
     assert line["ms_per_step"] == pytest.approx(max(line["rank_wall_s"]) / line["steps"] * 1e3, rel=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(420)
+def test_bench_configs3_eight_ranks_on_one_gpu():
+    """BASELINE configs[3] as the driver's 8-GPU run shards it: 1024 RS(29,80)
+    64 MiB segments per step, 128 per rank, contiguous shards, no data-path
+    collective.  Here all eight ranks share the box's one GPU (gloo for the
+    barrier and the max over ranks; the driver's run uses RCCL, one GPU per
+    rank); every rank encodes and rebuilds its own 128 segments and checks
+    them, and the rank-0 line reports the whole job."""
+    import json
+    import subprocess
+    import sys
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "8", "--steps",
+           "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline", "--no-other-configs"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["verified"] is True
+    assert line["config"]["total_segments_per_step"] == 1024 and line["config"]["segments_this_rank"] == 128
+    assert line["ranks_seen"] == 8 and len(line["rank_wall_s"]) == 8
+    assert line["value"] > 0
