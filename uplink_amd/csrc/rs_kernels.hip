@@ -142,6 +142,50 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     }
 }
 
+// Rebuild with nothing to compute (every data share present): a copy of the
+// data shares into the stripe-major segment, with no bit planes or barriers.
+// Each of the 2 waves loads all of its (up to 16) inputs of the tile before
+// it stores any, and the launch asks for kCopyLds bytes of LDS it never
+// touches, so only 2 workgroups share a CU: RS(29,80) 23.8 us per segment,
+// against 24.8-24.9 through rs_matmul_jt and 26.0-26.3 for this kernel at
+// full occupancy (more workgroups per CU, more write streams open at once;
+// DESIGN.md §4 "Rebuild, round 3").
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void rs_copy_shares(const RsArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int G = 16;
+    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const int64_t seg = tile / a.tiles_per_seg;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
+        uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
+        const int64_t oA = c.vA ? c.inA : 0, oB = c.vB ? c.inB : 0;
+        for (int j0 = wave; j0 < a.nin; j0 += NW * G) {
+            uint4 A[G], B[G];
+#pragma unroll
+            for (int i = 0; i < G; i++) {
+                const int j = j0 + NW * i;
+                if (j < a.nin) {
+                    const uint8_t *p = in_seg + a.in_off[j];
+                    const uint4 z = make_uint4(0, 0, 0, 0);
+                    A[i] = in_range(a, p + oA, false, 6) ? ld16<true>(p + oA) : z;
+                    B[i] = in_range(a, p + oB, false, 6) ? ld16<true>(p + oB) : z;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < G; i++) {
+                const int j = j0 + NW * i;
+                if (j < a.nin && a.copy_off[j] >= 0) {
+                    uint8_t *p = out_seg + a.copy_off[j];
+                    if (c.vA && in_range(a, p + c.outA, true, 7)) st16<true>(p + c.outA, A[i].x, A[i].y, A[i].z, A[i].w);
+                    if (c.vB && in_range(a, p + c.outB, true, 7)) st16<true>(p + c.outB, B[i].x, B[i].y, B[i].z, B[i].w);
+                }
+            }
+        }
+    }
+}
+
 template <int NW>
 size_t jt_lds_bytes(const RsArgs &) {
     return (size_t)2 * 2 * NW * 8 * 64 * 4;
@@ -270,6 +314,11 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     // per segment).  The encoder keeps its persistent grid (one
     // workgroup per tile: 809 -> 1248 us).
     if (grid <= 0) grid = (int)std::min<int64_t>(std::max<int64_t>(a.total_tiles, 1), 1 << 30);
+    if (a.nout == 0 && !a.zero_check) {
+        constexpr size_t kCopyLds = 58 * 1024;  // an occupancy cap: 2 workgroups per CU
+        hipLaunchKernelGGL(rs_copy_shares<2>, dim3(grid), dim3(2 * 64), kCopyLds, s, a);
+        return hipGetLastError();
+    }
     switch (SL ? sl::split_for(a.nout).nw : jt_waves(a.nout)) {
     case 8:
         hipLaunchKernelGGL((rs_matmul_jt<8, true>), dim3(grid), dim3(8 * 64), jt_lds_bytes<8>(a), s, a);
