@@ -390,7 +390,10 @@ def main():
     # device, host-side collectives); the driver's multi-GPU runs use the default, RCCL.
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     coll_dev = torch.device("cpu") if backend == "gloo" else None
-    if world > 1:
+    # BENCH_FORCE_DIST=1 (under torch.distributed.run) makes the process group and runs the bench's
+    # collectives even at world size 1, so a one-GPU box exercises the RCCL path the 8-GPU run takes
+    use_dist = world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1"
+    if use_dist:
         import torch.distributed as dist
         torch.cuda.set_device(local if backend != "gloo" else local % torch.cuda.device_count())
         if backend == "gloo":
@@ -439,7 +442,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if use_dist:
             import torch.distributed as dist
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -499,7 +502,7 @@ def main():
         by_set.setdefault(i, []).append(e[1].elapsed_time(e[2]) * 1e3 / B)
     # every rank's wall time (shard imbalance shows here) and a count of the ranks that took part
     rank_walls, ranks_seen = [round(wall, 6)], 1
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
         walls = [torch.zeros(1, dtype=torch.float64, device=coll_dev or dev) for _ in range(world)]
         dist.all_gather(walls, torch.tensor([wall], dtype=torch.float64, device=coll_dev or dev))
@@ -551,7 +554,7 @@ def main():
     encode(0, B)
     verified = verified and bool(torch.equal(par, pieces[0][:, K:]))
     del par
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
         v = torch.tensor([1 if verified else 0], device=coll_dev or dev)
         dist.all_reduce(v, op=dist.ReduceOp.MIN)
@@ -648,6 +651,7 @@ def main():
         "gpu_busy_s": round(t_enc + t_dec, 4),
         "segments_timed_this_rank": seg_launched,
         "ranks_seen": ranks_seen,
+        "collectives": backend if use_dist else None,
         "rank_wall_s": rank_walls,
         "build_id": L.ec_build_id().decode(),
         "verified": verified,
@@ -662,7 +666,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     L.ec_destroy(ctx)
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
         dist.destroy_process_group()
 

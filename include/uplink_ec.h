@@ -163,6 +163,23 @@ int ec_rebuild_segments_host(const ec_ctx *ctx, int nshares, const int *nums, co
  * when the piece hash algorithm is BLAKE3 (the default, piecestore/hash.go:20-26). */
 int ec_encode_segments_host_hashed(const ec_ctx *ctx, const uint8_t *segs, size_t nseg, size_t nstripes,
                                    uint8_t *pieces, uint8_t *hashes, int flags);
+/* Streamed form for one segment, for piece readers that serve each piece
+ * stripe by stripe as the reference does (segmentupload/encode.go:39-75,
+ * pieceReader.PieceReader single.go:228-238): the segment goes through the
+ * engine in chunks of stripes (chunk_stripes, or 0 for the library's choice:
+ * 128 stripes first, doubling up to 2048) and each chunk of every piece is in
+ * `pieces` (host, [rows][nstripes*ess] as ec_encode_segments_host) as soon as
+ * it is encoded.  ec_upload_begin queues everything and returns;
+ * ec_upload_wait blocks until stripes [0, stripes) of every piece are in host
+ * memory; ec_upload_ready returns how many leading stripes are, without
+ * blocking; ec_upload_end waits for the rest, frees the handle and returns the
+ * first error.  The caller keeps seg and pieces alive until ec_upload_end. */
+typedef struct ec_upload ec_upload;
+int ec_upload_begin(const ec_ctx *ctx, const uint8_t *seg, size_t nstripes, uint8_t *pieces, int flags,
+                    size_t chunk_stripes, ec_upload **out);
+int ec_upload_wait(ec_upload *u, size_t stripes);
+size_t ec_upload_ready(ec_upload *u);
+int ec_upload_end(ec_upload *u);
 void *ec_host_alloc(size_t bytes); /* pinned (hipHostMalloc); NULL on failure */
 void ec_host_free(void *p);
 

@@ -129,3 +129,32 @@ def test_bench_configs3_eight_ranks_on_one_gpu():
     assert line["config"]["total_segments_per_step"] == 1024 and line["config"]["segments_this_rank"] == 128
     assert line["ranks_seen"] == 8 and len(line["rank_wall_s"]) == 8
     assert line["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rccl_branch_at_world_one():
+    """the RCCL branch the driver's 8-GPU run takes --
+    init_process_group("nccl", device_id=...), the barriers, the device-tensor
+    all_gather of the wall times and the all_reduce of the rank count and the
+    verification flag -- run here on one GPU: bench.py under torch.distributed.run
+    with one rank and BENCH_FORCE_DIST=1 (no BENCH_DIST_BACKEND: RCCL)."""
+    import json
+    import subprocess
+    import sys
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BENCH_FORCE_DIST="1")
+    env.pop("BENCH_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "1", "--steps",
+           "2", "--warmup", "1", "--settle-s", "0", "--total-segments", "32", "--no-cpu-baseline",
+           "--no-other-configs"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["collectives"] == "nccl"
+    assert line["n_gpus"] == 1 and line["verified"] is True
+    assert line["ranks_seen"] == 1 and len(line["rank_wall_s"]) == 1
+    assert line["config"]["segments_this_rank"] == 32

@@ -109,3 +109,75 @@ def test_chunked_host_pipelines(oracle, k, n, ess, stripes, nseg):
     out2 = np.zeros((nseg, spad), dtype=np.uint8)
     assert lib.ec_rebuild_segments_host(sch.ctx, k, c_nums2, c_ptrs2, stripes, nseg, plen, out2.ctypes.data) == 0
     assert np.array_equal(out2, segs)
+
+
+@pytest.mark.parametrize("chunk", [0, 1, 7, 300, 100000])
+def test_streamed_parity_pieces_read_in_small_reads(oracle, chunk):
+    """the parity pieces arrive chunk by chunk
+    (ec_upload_begin) and a piece reader waits only for the chunk holding
+    the bytes it is asked for.  Pieces read in ragged small reads that cross
+    chunk and stripe boundaries, interleaved over pieces, equal the oracle's;
+    data pieces are gathered per read from the segment."""
+    k, n, ess = 29, 80, 256
+    rs = _rs(k, n, ess)
+    size = 2 * 1024 * 1024 + 777
+    data = np.random.default_rng(chunk + 1).integers(0, 256, size, dtype=np.uint8).tobytes()
+    padded = eestream.pad(data, rs.stripe_size())
+    ref = oracle.FEC(k, n).encode_segment(np.frombuffer(padded, dtype=np.uint8), ess)
+    spr = segment.SegmentPieceReader(data, rs, chunk_stripes=chunk)
+    readers = {num: spr.piece_reader(num) for num in (0, 5, 28, 29, 30, 54, 79)}
+    got = {num: [] for num in readers}
+    plen = ref.shape[1]
+    rng = np.random.default_rng(3)
+    left = set(readers)
+    while left:
+        for num in sorted(left):
+            b = readers[num].read(int(rng.integers(1, 3000)))
+            if not b:
+                left.discard(num)
+            got[num].append(b)
+    for num in readers:
+        assert b"".join(got[num]) == ref[num].tobytes(), num
+    assert spr.ready_stripes() == plen // ess
+    spr.close()
+    with pytest.raises(eestream.EEStreamError):
+        spr._wait(1)
+
+
+def test_streamed_upload_c_abi_partial_wait_and_threads(oracle):
+    """ec_upload_wait(u, s) returns once stripes [0, s) of every piece are in
+    host memory -- checked right after each wait, before the upload ends --
+    for the full (all n pieces) and parity-only layouts, from 8 threads
+    waiting on one upload at once; argument errors."""
+    import ctypes
+    import threading
+    from uplink_amd import _native as NAT
+    lib = NAT.load()
+    k, n, ess, stripes = 29, 80, 256, 3000
+    sch = eestream.RSScheme(eestream.new_fec(k, n), ess)
+    seg = np.random.default_rng(9).integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    assert lib.ec_upload_begin(sch.ctx, None, stripes, None, 0, 0, ctypes.byref(ctypes.c_void_p())) \
+        == NAT.EC_ERR_INVALID_ARG
+    assert lib.ec_upload_wait(None, 1) == NAT.EC_ERR_INVALID_ARG
+    for flags, rows in ((0, n), (NAT.EC_FLAG_PARITY_ONLY, n - k)):
+        pieces = segment.PinnedHost(rows * stripes * ess)
+        view = pieces.array.reshape(rows, stripes * ess)
+        h = ctypes.c_void_p()
+        assert lib.ec_upload_begin(sch.ctx, seg.ctypes.data, stripes, pieces.ptr, flags, 0, ctypes.byref(h)) == 0
+        errors = []
+
+        def waiter(t):
+            s = (t + 1) * stripes // 8
+            if lib.ec_upload_wait(h, s) != 0:
+                errors.append((t, "rc"))
+            elif not np.array_equal(view[:, : s * ess], ref[n - rows:, : s * ess]):
+                errors.append((t, s))
+        th = [threading.Thread(target=waiter, args=(t,)) for t in range(8)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        assert not errors, errors
+        assert lib.ec_upload_ready(h) == stripes
+        assert lib.ec_upload_end(h) == 0
+        assert np.array_equal(view, ref[n - rows:])
+        pieces.close()

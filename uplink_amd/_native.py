@@ -85,6 +85,11 @@ SIGNATURES = {
     "ec_gcm_seal_host": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp]),
     "ec_gcm_open_host": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp,
                                         ctypes.POINTER(ctypes.c_longlong)]),
+    "ec_upload_begin": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_int, ctypes.c_size_t,
+                                       ctypes.POINTER(vp)]),
+    "ec_upload_wait": (ctypes.c_int, [vp, ctypes.c_size_t]),
+    "ec_upload_ready": (ctypes.c_size_t, [vp]),
+    "ec_upload_end": (ctypes.c_int, [vp]),
     "ec_host_alloc": (vp, [ctypes.c_size_t]),
     "ec_host_free": (None, [vp]),
     "ec_device_count": (ctypes.c_int, []),

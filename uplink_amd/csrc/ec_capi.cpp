@@ -200,18 +200,32 @@ struct HostPipe {
     size_t in_cap = 0, out_cap = 0;
 };
 
+// Device side of one streamed upload (ec_upload_begin): the segment, its
+// pieces and the three role streams (H2D, encode, D2H).  Kept in a per-context
+// pool between uploads; one upload owns a slot from begin to end.
+struct UploadSlot {
+    hipStream_t st[3] = {};
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    size_t in_cap = 0, out_cap = 0;
+    std::vector<hipEvent_t> ev;  // [in ch][enc ch][d2h ch] of the current upload
+};
+
 // Work counters of the compile-time encoder's launches (RsArgs::queue): a
-// ring of counters, each zeroed on the launch's stream right before it and
-// handed to no other launch until an event behind its last launch has
-// completed, so launches on different streams never share one.
+// ring of counter pairs (tile counter, workgroups done), zeroed once when the
+// ring is made.  The last workgroup of a launch puts its pair back to zero
+// (rs_encoder.hpp), so a launch needs no memset before it.  A slot serves one
+// launch at a time: it goes to a launch on the stream its previous launch ran
+// on (stream order), or to any stream once the event behind its previous
+// launch has completed; with no such slot the launch assigns its tiles
+// statically (identical results).  No launch waits on another stream.
 struct QueueRing {
     static constexpr int kSlots = 32;
-    static constexpr int kStride = 64;  // words: one counter per 256 bytes
+    static constexpr int kStride = 64;  // words per slot: the counter pair (kQueueDoneWord), a slot per 256 bytes
     std::mutex mu;
     uint32_t *d = nullptr;
     hipEvent_t ev[kSlots] = {};
+    hipStream_t owner[kSlots] = {};  // stream of the slot's last launch
     bool used[kSlots] = {}, busy[kSlots] = {};
-    int next = 0;
 };
 
 struct ec_ctx {
@@ -219,6 +233,8 @@ struct ec_ctx {
     QueueRing qring;
     std::mutex pipe_mu;  // one host pipeline at a time per context
     HostPipe pipe;
+    std::mutex upload_mu;
+    std::vector<std::unique_ptr<UploadSlot>> upload_free;  // idle streamed-upload slots
     std::vector<uint8_t> G;        // n x k
     hipStream_t setup = nullptr;   // plan uploads (synchronous, never a caller's stream)
     std::shared_ptr<DevArena> arena = std::make_shared<DevArena>();
@@ -238,6 +254,10 @@ struct ec_ctx {
     std::mutex single_mu;
     std::deque<SingleReq *> single_q;
     int single_leaders = 0;
+    // fault injection for tests only (UPLINK_EC_FAULT_SINGLE="max=M,num=J" read
+    // at ec_create): EncodeSingle batches of more than M requests find no
+    // staging, nor does a one-request batch for share J
+    int fault_max_batch = 0, fault_fail_num = -1;
 };
 
 namespace {
@@ -491,39 +511,48 @@ int after_launch(uint32_t *chk, hipStream_t s) {
 }
 
 // A zeroed work counter for one encoder launch on stream s (slot in *slot;
-// queue_done after the launch).  nullptr when none can be had: the kernel then
-// assigns its tiles statically, with identical results.
+// queue_done after the launch).  nullptr when none can be had without waiting
+// for another stream: the kernel then assigns its tiles statically, with
+// identical results.  (A stream handle is taken to name one stream while work
+// queued on it is in flight.)
 uint32_t *queue_take(ec_ctx *c, hipStream_t s, int *slot) {
     QueueRing &q = c->qring;
     std::lock_guard<std::mutex> g(q.mu);
     if (!q.d) {
-        if (hipMalloc(&q.d, sizeof(uint32_t) * QueueRing::kStride * QueueRing::kSlots) != hipSuccess) {
+        const size_t bytes = sizeof(uint32_t) * QueueRing::kStride * QueueRing::kSlots;
+        if (hipMalloc(&q.d, bytes) != hipSuccess) {
+            q.d = nullptr;
+            return nullptr;
+        }
+        if (hipMemset(q.d, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(q.d);
             q.d = nullptr;
             return nullptr;
         }
         for (int i = 0; i < QueueRing::kSlots; i++)
             if (hipEventCreateWithFlags(&q.ev[i], hipEventDisableTiming) != hipSuccess) q.ev[i] = nullptr;
     }
-    for (int tries = 0; tries < QueueRing::kSlots; tries++) {
-        const int i = q.next;
-        q.next = (q.next + 1) % QueueRing::kSlots;
-        if (q.busy[i] || !q.ev[i]) continue;
-        // the slot's previous launch (any stream) is done before this one zeroes it
-        if (q.used[i] && hipStreamWaitEvent(s, q.ev[i], 0) != hipSuccess) continue;
-        uint32_t *ctr = q.d + (size_t)i * QueueRing::kStride;
-        if (hipMemsetAsync(ctr, 0, sizeof(uint32_t), s) != hipSuccess) continue;
-        q.busy[i] = true;
-        *slot = i;
-        return ctr;
-    }
-    return nullptr;
+    int pick = -1;
+    // the slot this stream used last: its previous launch precedes this one in stream order
+    for (int i = 0; i < QueueRing::kSlots && pick < 0; i++)
+        if (q.used[i] && !q.busy[i] && q.owner[i] == s && q.ev[i]) pick = i;
+    // else a fresh slot, or one whose last launch (on another stream) has completed
+    for (int i = 0; i < QueueRing::kSlots && pick < 0; i++)
+        if (!q.busy[i] && q.ev[i] && (!q.used[i] || hipEventQuery(q.ev[i]) == hipSuccess)) pick = i;
+    if (pick < 0) return nullptr;
+    q.busy[pick] = true;
+    *slot = pick;
+    return q.d + (size_t)pick * QueueRing::kStride;
 }
 
-void queue_done(ec_ctx *c, hipStream_t s, int slot) {
+void queue_done(ec_ctx *c, hipStream_t s, int slot, bool launched) {
     QueueRing &q = c->qring;
     std::lock_guard<std::mutex> g(q.mu);
-    q.used[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
-    if (!q.used[slot]) (void)hipStreamSynchronize(s);  // no event: let the launch finish before the slot returns
+    if (launched) {
+        q.used[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
+        if (!q.used[slot]) (void)hipStreamSynchronize(s);  // no event: let the launch finish before the slot returns
+        q.owner[slot] = s;
+    }
     q.busy[slot] = false;
 }
 
@@ -774,6 +803,8 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     HIP_TRY(hipMalloc(&c->d_chk, 4));
     HIP_TRY(hipMemset(c->d_chk, 0, 4));
 #endif
+    if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
+        if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;
     *out = c.release();
     return EC_OK;
 }
@@ -786,6 +817,15 @@ void ec_destroy(ec_ctx *c) {
         if (c->pipe.d_in[s]) (void)hipFree(c->pipe.d_in[s]);
         if (c->pipe.d_out[s]) (void)hipFree(c->pipe.d_out[s]);
     }
+    for (auto &u : c->upload_free) {
+        for (auto st : u->st)
+            if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
+        for (auto e : u->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (u->d_in) (void)hipFree(u->d_in);
+        if (u->d_out) (void)hipFree(u->d_out);
+    }
+    c->upload_free.clear();
     for (auto &w : c->all_ws) {
         if (w->stream) (void)hipStreamSynchronize(w->stream), (void)hipStreamDestroy(w->stream);
         if (w->d_buf) (void)hipFree(w->d_buf);
@@ -905,7 +945,7 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
             int slot = -1;
             a.queue = queue_take(c, s, &slot);
             const hipError_t e = launch_encode_special(*ek, a, 0, s);
-            if (slot >= 0) queue_done(c, s, slot);
+            if (slot >= 0) queue_done(c, s, slot, e == hipSuccess);
             HIP_TRY(e);
             return after_launch(c->d_chk, s);
         }
@@ -975,28 +1015,45 @@ static int pipe_drain(ec_ctx *c, int rc) {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // ---------------------------------------------------------------- per-stripe
+// single_batch_once: one launch sequence for the whole batch, or kSplit when
+// the staging for it cannot be had (and the batch has more than one request)
+constexpr int kSplit = 1;
+static int single_batch_once(ec_ctx *c, SingleReq *const *req, size_t nreq, size_t bs);
+
 // One launch sequence for EncodeSingle requests of one share size bs: the
 // stripes are packed into pinned staging, copied in with one transfer, the
 // parity of every stripe is encoded in one launch (the compile-time encoder
 // where there is one), a gather kernel picks each request's share, and one
-// transfer brings them back.
-static int run_single_batch(ec_ctx *c, SingleReq *const *req, size_t nreq, size_t bs) {
+// transfer brings them back.  Sets every request's rc: the outcome of the
+// launch sequence that carried it (a batch split for want of staging carries
+// each half on its own, and each half's requests get that half's outcome).
+static void run_single_batch(ec_ctx *c, SingleReq *const *req, size_t nreq, size_t bs) {
+    const int rc = single_batch_once(c, req, nreq, bs);
+    if (rc == kSplit) {
+        // no room for the whole batch: each half on its own (a request that
+        // would succeed alone does not fail for sharing a batch)
+        const size_t h = nreq / 2;
+        run_single_batch(c, req, h, bs);
+        run_single_batch(c, req + h, nreq - h, bs);
+        return;
+    }
+    for (size_t r = 0; r < nreq; r++) req[r]->rc = rc;
+}
+
+static int single_batch_once(ec_ctx *c, SingleReq *const *req, size_t nreq, size_t bs) {
     const int k = c->k, n = c->n;
     const size_t stripe = (size_t)k * bs;
     const size_t in_bytes = nreq * stripe, par_bytes = (size_t)(n - k) * nreq * bs, out_bytes = nreq * bs;
     // device: [stripes | nums | parity | out]; pinned host: [stripes | nums | out]
     const size_t nums_at = align_up(in_bytes, 256), par_at = nums_at + align_up(nreq * 4, 256);
     const size_t out_at = par_at + align_up(par_bytes, 256), h_out = par_at;
+    if (c->fault_max_batch > 0 &&
+        (nreq > (size_t)c->fault_max_batch || (nreq == 1 && req[0]->num == c->fault_fail_num)))
+        return nreq == 1 ? EC_ERR_DEVICE : kSplit;  // (test hook, see ec_ctx)
     Workspace *w = acquire_ws(c, out_at + out_bytes + 64, h_out + out_bytes);
     if (!w->d_buf || !w->stream || !w->h_buf) {
         release_ws(c, w);
-        if (nreq == 1) return EC_ERR_DEVICE;
-        // no room for the whole batch: each half on its own (a request that
-        // would succeed alone does not fail for sharing a batch)
-        const size_t h = nreq / 2;
-        const int r1 = run_single_batch(c, req, h, bs), r2 = run_single_batch(c, req + h, nreq - h, bs);
-        for (size_t r = 0; r < h; r++) req[r]->rc = r1;
-        return r2;
+        return nreq == 1 ? EC_ERR_DEVICE : kSplit;
     }
     for (size_t r = 0; r < nreq; r++) {
         memcpy(w->h_buf + r * stripe, req[r]->in, stripe);
@@ -1105,10 +1162,7 @@ int ec_encode_single(const ec_ctx *cc, const uint8_t *in, size_t in_len, uint8_t
         for (size_t i = 0; i < batch.size();) {
             size_t j = i;
             while (j < batch.size() && batch[j]->bs == batch[i]->bs) j++;
-            for (size_t q = i; q < j; q++) batch[q]->rc = EC_OK;
-            const int rc = run_single_batch(c, batch.data() + i, j - i, batch[i]->bs);
-            for (size_t q = i; q < j; q++)
-                if (batch[q]->rc == EC_OK) batch[q]->rc = rc;
+            run_single_batch(c, batch.data() + i, j - i, batch[i]->bs);  // sets each request's rc
             i = j;
         }
         lk.lock();
@@ -1345,6 +1399,150 @@ int ec_encode_segments_host_hashed(const ec_ctx *cc, const uint8_t *segs, size_t
                                    uint8_t *pieces, uint8_t *hashes, int flags) {
     if (!hashes) return EC_ERR_INVALID_ARG;
     return encode_host(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, pieces, hashes, flags);
+}
+
+// ---------------------------------------------------------------- streamed upload
+// One segment through the engine in chunks of stripes, each chunk of every
+// piece in host memory as soon as it is encoded, for piece readers that serve
+// a piece stripe by stripe (segmentupload/encode.go:39-75, single.go:228-238):
+// an upload starts sending after the first chunk instead of the whole segment.
+// Chunks grow from kUploadFirstChunk stripes, doubling up to kUploadMaxChunk,
+// so the first bytes come early and the later chunks keep the PCIe pipeline
+// (H2D of chunk i+1, encode of chunk i, D2H of chunk i-1) busy.
+constexpr size_t kUploadFirstChunk = 128, kUploadMaxChunk = 2048;
+
+struct ec_upload {
+    ec_ctx *c = nullptr;
+    std::unique_ptr<UploadSlot> slot;
+    std::vector<size_t> end;  // end stripe of each chunk
+    std::atomic<int> rc{EC_OK};
+    std::atomic<int> done{0};  // leading chunks known to be in host memory
+};
+
+static void upload_release(ec_upload *u) {
+    if (!u->slot) return;
+    for (auto st : u->slot->st)
+        if (st) (void)hipStreamSynchronize(st);
+    std::lock_guard<std::mutex> g(u->c->upload_mu);
+    u->c->upload_free.push_back(std::move(u->slot));
+}
+
+int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8_t *pieces, int flags,
+                    size_t chunk_stripes, ec_upload **out) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!out) return EC_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!c || !seg || !pieces) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    std::unique_ptr<ec_upload> u(new ec_upload());
+    u->c = c;
+    for (size_t s0 = 0, len = chunk_stripes ? chunk_stripes : kUploadFirstChunk; s0 < nstripes;) {
+        const size_t s1 = std::min(nstripes, s0 + len);
+        u->end.push_back(s1);
+        s0 = s1;
+        if (!chunk_stripes) len = std::min(kUploadMaxChunk, 2 * len);
+    }
+    const size_t nch = u->end.size();
+    const size_t ess = c->ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
+    const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
+    const int rows = parity_only ? c->n - c->k : c->n;
+    const size_t plen = nstripes * ess, pbytes = (size_t)rows * plen;
+    {
+        std::lock_guard<std::mutex> g(c->upload_mu);
+        if (!c->upload_free.empty()) {
+            u->slot = std::move(c->upload_free.back());
+            c->upload_free.pop_back();
+        }
+    }
+    if (!u->slot) u->slot.reset(new UploadSlot());
+    UploadSlot &sl = *u->slot;
+    for (auto &st : sl.st)
+        if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (sl.in_cap < spad) {
+        if (sl.d_in) (void)hipFree(sl.d_in);
+        sl.d_in = nullptr;
+        sl.in_cap = 0;
+        HIP_TRY(hipMalloc(&sl.d_in, std::max<size_t>(spad, 1)));
+        sl.in_cap = spad;
+    }
+    if (sl.out_cap < pbytes) {
+        if (sl.d_out) (void)hipFree(sl.d_out);
+        sl.d_out = nullptr;
+        sl.out_cap = 0;
+        HIP_TRY(hipMalloc(&sl.d_out, std::max<size_t>(pbytes, 1)));
+        sl.out_cap = pbytes;
+    }
+    while (sl.ev.size() < 3 * nch) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        sl.ev.push_back(e);
+    }
+    hipStream_t h2d = sl.st[0], comp = sl.st[1], d2h = sl.st[2];
+    int rc = EC_OK;
+    for (size_t ch = 0; ch < nch && rc == EC_OK; ch++) {
+        const size_t s0 = ch ? u->end[ch - 1] : 0, s1 = u->end[ch];
+        hipEvent_t e_in = sl.ev[ch], e_enc = sl.ev[nch + ch], e_out = sl.ev[2 * nch + ch];
+        if (hipMemcpyAsync(sl.d_in + s0 * stripe, seg + s0 * stripe, (s1 - s0) * stripe, hipMemcpyHostToDevice,
+                           h2d) != hipSuccess ||
+            hipEventRecord(e_in, h2d) != hipSuccess || hipStreamWaitEvent(comp, e_in, 0) != hipSuccess) {
+            rc = EC_ERR_DEVICE;
+            break;
+        }
+        if (rows > 0) rc = encode_range(c, sl.d_in, 1, nstripes, s0, s1, sl.d_out, flags, comp);
+        if (rc) break;
+        if (hipEventRecord(e_enc, comp) != hipSuccess || hipStreamWaitEvent(d2h, e_enc, 0) != hipSuccess ||
+            (rows > 0 && hipMemcpy2DAsync(pieces + s0 * ess, plen, sl.d_out + s0 * ess, plen, (s1 - s0) * ess, rows,
+                                          hipMemcpyDeviceToHost, d2h) != hipSuccess) ||
+            hipEventRecord(e_out, d2h) != hipSuccess)
+            rc = EC_ERR_DEVICE;
+    }
+    u->rc.store(rc);
+    if (rc) {
+        upload_release(u.get());
+        return rc;
+    }
+    *out = u.release();
+    return EC_OK;
+}
+
+// Any number of threads may wait on one upload (one per piece reader); the
+// event waits run without a lock, and the count of done chunks only grows.
+int ec_upload_wait(ec_upload *u, size_t stripes) {
+    if (!u) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(u->c->device);
+    const int nch = (int)u->end.size();
+    for (;;) {
+        if (const int rc = u->rc.load()) return rc;
+        int d = u->done.load();
+        if (d == nch || (d > 0 && u->end[d - 1] >= stripes)) return EC_OK;
+        if (hipEventSynchronize(u->slot->ev[2 * nch + d]) != hipSuccess) {
+            u->rc.store(EC_ERR_DEVICE);
+            return EC_ERR_DEVICE;
+        }
+        u->done.compare_exchange_strong(d, d + 1);
+    }
+}
+
+size_t ec_upload_ready(ec_upload *u) {
+    if (!u || u->rc.load()) return 0;
+    DeviceGuard dg(u->c->device);
+    const int nch = (int)u->end.size();
+    for (int d = u->done.load(); d < nch && hipEventQuery(u->slot->ev[2 * nch + d]) == hipSuccess; d = u->done.load())
+        u->done.compare_exchange_strong(d, d + 1);
+    const int d = u->done.load();
+    return d ? u->end[d - 1] : 0;
+}
+
+int ec_upload_end(ec_upload *u) {
+    if (!u) return EC_ERR_INVALID_ARG;
+    int rc = u->rc.load();
+    {
+        DeviceGuard dg(u->c->device);
+        if (rc == EC_OK) rc = ec_upload_wait(u, SIZE_MAX);
+        upload_release(u);
+    }
+    delete u;
+    return rc;
 }
 
 int ec_hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,

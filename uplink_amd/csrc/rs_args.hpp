@@ -10,6 +10,11 @@ namespace uplink_ec {
 // the rows computed).  Larger row counts are split over several launches.
 constexpr int kMaxOps = 128;
 
+// RsArgs::queue points at a pair of counters: the launch's tile counter at
+// word 0 and, at this word, the count of its workgroups that are done; both
+// are zero when a launch starts, and its last workgroup zeroes them again.
+constexpr int kQueueDoneWord = 32;
+
 // One launch computes, for every byte column (stripe s, offset t < ess) of
 // every segment g in the batch:
 //   out_r[g, s, t] = XOR_j  M[r][j] * in_j[g, s, t]      (GF(2^8))
@@ -43,7 +48,7 @@ struct RsArgs {
     // paired across the batch (rs_tile.hpp pair_cols), handed out by a queue
     int64_t blocks_per_seg;   // ceil(chunks_per_seg / 64)
     int64_t total_blocks;     // blocks_per_seg * nseg
-    uint32_t *queue;          // zeroed work counter of this launch (null: static assignment)
+    uint32_t *queue;          // zero work counters of this launch, see kQueueDoneWord (null: static assignment)
     // runtime-matrix kernel: when set, the computed rows are checked for zero
     // instead of stored (syndrome rows of ec_decode_segments); each wave that
     // finds a non-zero byte in a valid column adds 1 here
@@ -60,6 +65,7 @@ struct RsArgs {
     const uint8_t *chk_in_lo, *chk_in_hi;
     const uint8_t *chk_out_lo, *chk_out_hi;
     uint32_t *chk_flag;       // checked build: first violating site (0 = none)
+    uint64_t *diag;           // diagnostic encoder forms only (rs_encoder.hpp kDiagStamp); null otherwise
     int64_t in_off[kMaxOps];  // bytes from in_base (16-byte aligned on the bit-sliced path)
     int64_t out_off[kMaxOps]; // bytes from out_base
     int64_t copy_off[kMaxOps];// bytes from out_base, -1 = no copy

@@ -58,7 +58,7 @@ constexpr int rbase_of(int R, int NC, int W) { return W * (R / NC) + (W < R % NC
 // acc[O] ^= G[K + rbase + O][J] * x_J for the wave's rows and the inputs
 // J0 .. J0+JN-1, whose bit planes sit at slot position J - J0 (planes 0-3 of a
 // lane as one 16-byte word at 16 lane, planes 4-7 at 1024 + 16 lane).
-template <int K, int N, int NC, int OPW, int W, int J0, int JN>
+template <int K, int N, int NC, int OPW, int W, int J0, int JN, int DIAG = 0>
 __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint32_t (&acc)[OPW][8]) {
     // The plane reads are the same in every wave's arm of the caller's switch;
     // an offset the compiler cannot see through keeps it from hoisting them out
@@ -77,6 +77,10 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
         }
         asm volatile("" ::: "memory");
         const uint32_t x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+        if constexpr ((DIAG & 16) != 0) {  // kDiagNoRowOps
+            asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+            return;
+        }
         uint32_t lo[16], hi[16];
         lo[0] = 0;
         hi[0] = 0;
@@ -84,7 +88,7 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
             constexpr int M = M1 + 1;
             constexpr int low = M & (-M);
             constexpr int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
-            if constexpr (M == low) {
+            if constexpr (M == low || (DIAG & 8) != 0) {  // (kDiagNoCombos: every entry a single plane)
                 lo[M] = x[bit];
                 hi[M] = x[4 + bit];
             } else {
@@ -112,8 +116,8 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
 }
 
 // Tile for the m-th take of this workgroup: from the launch's work queue
-// (a.queue, zeroed before the launch) or, without one, statically.  Only one
-// lane calls it; a returning vector atomic, not a scalar one.
+// (a.queue, zero when the launch starts) or, without one, statically.  Only
+// one lane calls it; a returning vector atomic, not a scalar one.
 __device__ __forceinline__ int32_t take_tile(const RsArgs &a, int m) {
     if (a.queue) return (int32_t)atomicAdd(a.queue, 1u);
     return (int32_t)(blockIdx.x + (int64_t)m * gridDim.x);
@@ -137,10 +141,31 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
+// Diagnostic forms of the encoder body (DIAG != 0), instantiated only by the
+// measurement harness tools/exp/enc_diag.hip, never by the library:
+//   kDiagStamp            wave 0 of every workgroup stamps s_memtime and
+//                         s_memrealtime around its tile loop, and compute wave 0
+//                         and loader wave 0 count the cycles they spend waiting
+//                         (barriers; the loader's counted vmcnt waits), into
+//                         a.diag[8 * blockIdx.x ..]; nothing else reads them
+//   kDiagNoParityStores   the parity rows are computed (and un-bit-sliced) but
+//                         handed to an empty asm that keeps them live, not stored
+//   kDiagNoCopyStores     the same for the loaders' copy-through of the data pieces
+//                         (their vmcnt waits then count no stores)
+//   kDiagNoCombos         timing only: the 22 combination planes per input are
+//                         not built (every combination reads a single plane)
+//   kDiagNoRowOps         timing only: no multiply-add at all (the inputs' planes
+//                         are read from the LDS and kept live, the rows stay zero)
+constexpr int kDiagStamp = 1, kDiagNoParityStores = 2, kDiagNoCopyStores = 4, kDiagNoCombos = 8, kDiagNoRowOps = 16;
+
+__device__ __forceinline__ void sink16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    asm volatile("" ::"v"(x), "v"(y), "v"(z), "v"(w));
+}
+
 // COPY: the full encode (the systematic data pieces written too); false: the
 // parity-only form (EC_FLAG_PARITY_ONLY), a kernel of its own name.
-template <int K, int N, int NC, int NL, bool COPY>
-__global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
+template <int K, int N, int NC, int NL, bool COPY, int DIAG>
+__device__ __forceinline__ void encode_body(const RsArgs &a) {
     constexpr int R = N - K;
     constexpr int OPW = (R + NC - 1) / NC;
     constexpr int NCH = chunks_of(K), KC = chunk_size(K);
@@ -175,8 +200,14 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
 #ifdef UPLINK_EC_CHECKED
     constexpr bool kCountStores = false;  // the checked build may skip a store: count none (waits longer, never shorter)
 #else
-    constexpr bool kCountStores = true;
+    constexpr bool kCountStores = !(DIAG & kDiagNoCopyStores);
 #endif
+    // kDiagStamp: cycles this wave spent waiting, and the stamps around the loop
+    [[maybe_unused]] uint64_t d_wait = 0, d_t0 = 0, d_r0 = 0;
+    auto d_now = [&]() -> uint64_t {
+        if constexpr ((DIAG & kDiagStamp) != 0) return __builtin_amdgcn_s_memtime();
+        return 0;
+    };
     // loader: LDS-DMA of this wave's inputs of item (t, ch) into slot sl
     auto issue = [&](int sl, int64_t t, int ch) {
         const TileCols c = pair_cols(a, t, lane);
@@ -212,7 +243,10 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
             const int j = lw + NL * i;
             if (j < jn) {
                 const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
-                if constexpr (do_copy) {
+                if constexpr (do_copy && (DIAG & kDiagNoCopyStores) != 0) {
+                    sink16(A4.x, A4.y, A4.z, A4.w);
+                    sink16(B4.x, B4.y, B4.z, B4.w);
+                } else if constexpr (do_copy) {
                     uint8_t *p = a.out_base + a.copy_off[j0 + j];
                     uint8_t *qa = p + (c.vA ? c.outA : 0), *qb = p + (c.vB ? c.outB : 0);
                     if (in_range(a, qa, true, 2)) st16<true>(qa, A4.x, A4.y, A4.z, A4.w);
@@ -231,6 +265,29 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
 #pragma unroll
         for (int m = 0; m < K0; m++) s_q[m] = take_tile(a, m);
     lds_barrier();
+    if constexpr ((DIAG & kDiagStamp) != 0) {
+        d_t0 = __builtin_amdgcn_s_memtime();
+        d_r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    // kDiagStamp: a barrier, its wait counted
+    auto barrier_w = [&]() {
+        const uint64_t t = d_now();
+        lds_barrier();
+        if constexpr ((DIAG & kDiagStamp) != 0) d_wait += d_now() - t;
+    };
+    // kDiagStamp: the stamps of wave w (compute wave 0 at slots 0-3, loader wave 0 at 4-7)
+    auto stamp_out = [&](int at) {
+        if constexpr ((DIAG & kDiagStamp) != 0) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0 && a.diag) {
+                uint64_t *d = a.diag + 8 * (int64_t)blockIdx.x + at;
+                d[0] = t1 - d_t0;
+                d[1] = r1 - d_r0;
+                d[2] = d_wait;
+                d[3] = 1;
+            }
+        }
+    };
     if (loader) {
         // items 0 .. A-1 in flight, item 0 bit-sliced
         int after = 0;
@@ -248,7 +305,7 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
             slice(0, t0, 0);
         }
     }
-    lds_barrier();
+    barrier_w();
     if (loader) {
         for (int i = 0;; i++) {
             if (tile_of(i) >= P) break;
@@ -268,11 +325,14 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
 #pragma unroll
                 for (int y = i + 2; y <= i + A; y++)
                     if (tile_of(y) < P) after += ops_of(y % NCH);
+                const uint64_t tw = d_now();
                 wait_vm(after);
+                if constexpr ((DIAG & kDiagStamp) != 0) d_wait += d_now() - tw;
                 slice((i + 1) % kSlots, u1, (i + 1) % NCH);
             }
-            lds_barrier();
+            barrier_w();
         }
+        if (lw == 0) stamp_out(4);
         return;
     }
     // compute waves: per tile, the chunks in order with a barrier after each (the
@@ -298,16 +358,35 @@ __global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsA
             constexpr int J0 = C * KC, JN = K - J0 < KC ? K - J0 : KC;
             const u32x4 *slot = ring + (i % kSlots) * (SLOT / 16);
             static_for<NC>([&]<int W>() {
-                if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN>(slot, lane, acc);
+                if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN, DIAG>(slot, lane, acc);
             });
             if (pend_m >= 0) s_q[pend_m & 7] = pending;
             if constexpr (C == NCH - 1) {
                 const TileCols c = pair_cols(a, ti, lane);
-                store_rows<OPW, true>(a, 0, c, rbase_of(R, NC, wave), rows_of(R, NC, wave), acc);
+                if constexpr ((DIAG & kDiagNoParityStores) != 0)
+                    sink_rows<OPW>(rows_of(R, NC, wave), acc);
+                else
+                    store_rows<OPW, true>(a, 0, c, rbase_of(R, NC, wave), rows_of(R, NC, wave), acc);
             }
-            lds_barrier();
+            barrier_w();
         });
     }
+    if (wave == 0) stamp_out(0);
+    // The launch's last workgroup to finish zeroes the queue for the next launch
+    // that gets it (so none needs a memset before it).  Every take of this
+    // workgroup has returned (its value was used above) before its done count
+    // is added, so when the count reaches gridDim.x no take of the launch is left.
+    if (taker && a.queue) {
+        if (atomicAdd(a.queue + kQueueDoneWord, 1u) == gridDim.x - 1) {
+            atomicExch(a.queue, 0u);
+            atomicExch(a.queue + kQueueDoneWord, 0u);
+        }
+    }
+}
+
+template <int K, int N, int NC, int NL, bool COPY>
+__global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
+    encode_body<K, N, NC, NL, COPY, 0>(a);
 }
 
 // Limits of the compile-time encoder: 1 <= n - k <= 96 parity rows (12

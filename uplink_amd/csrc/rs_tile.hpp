@@ -244,5 +244,20 @@ __device__ __forceinline__ void store_rows(const RsArgs &a, int64_t seg, const T
     });
 }
 
+// Diagnostic stand-in for store_rows (rs_encoder.hpp kDiagNoParityStores):
+// the rows are un-bit-sliced as for the store and kept live by an empty asm.
+template <int OPW>
+__device__ __forceinline__ void sink_rows(int cnt, uint32_t (&acc)[OPW][8]) {
+    static_for<OPW>([&]<int O>() {
+        if (O < cnt) {
+            uint32_t w[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) w[p] = acc[O][p];
+            unbitslice8(w);
+            asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]));
+        }
+    });
+}
+
 }  // namespace dev
 }  // namespace uplink_ec

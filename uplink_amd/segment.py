@@ -134,12 +134,41 @@ class PinnedBackend:
 
 
 class _PieceStream:
-    def __init__(self, src: np.ndarray):
-        self._src, self._off = src, 0
+    """io.ReadCloser over one piece.  `ready(end)` is called before bytes
+    [.., end) are read: for a parity piece of a streamed upload it blocks
+    until the stripes holding them are in host memory (ec_upload_wait)."""
+
+    def __init__(self, src: np.ndarray, ready=None):
+        self._src, self._off, self._ready = src, 0, ready
 
     def read(self, n: int = -1) -> bytes:
         end = self._src.size if n is None or n < 0 else min(self._src.size, self._off + n)
+        if self._ready is not None and end > self._off:
+            self._ready(end)
         b = self._src[self._off:end].tobytes()
+        self._off = end
+        return b
+
+    def close(self):
+        return None
+
+
+class _DataPieceStream:
+    """A data piece (num < k) is share num of every stripe of the padded
+    segment (EncodeSingle copies it, rs.go:21-23): gathered per read from the
+    host segment, with no engine call and nothing to wait for."""
+
+    def __init__(self, padded: np.ndarray, num: int):
+        self._p, self._num, self._off = padded, num, 0  # padded: [stripes][k][ess]
+        self._size = padded.shape[0] * padded.shape[2]
+
+    def read(self, n: int = -1) -> bytes:
+        end = self._size if n is None or n < 0 else min(self._size, self._off + n)
+        if end <= self._off:
+            return b""
+        ess = self._p.shape[2]
+        s0, s1 = self._off // ess, (end + ess - 1) // ess
+        b = self._p[s0:s1, self._num, :].reshape(-1)[self._off - s0 * ess:end - s0 * ess].tobytes()
         self._off = end
         return b
 
@@ -150,16 +179,25 @@ class _PieceStream:
 class SegmentPieceReader:
     """pieceReader (single.go:228-238): piece_reader(num) streams piece num
     of the segment (PadReader to the stripe size, then EncodeSingle per
-    stripe).  The first call pads and encodes the whole segment once."""
+    stripe).  The first call pads the segment once and starts one streamed
+    engine call for every parity piece (ec_upload_begin): the segment goes
+    through the GPU in chunks of stripes, and a parity piece's reader blocks
+    only until the chunk holding the bytes it is asked for has arrived, so an
+    upload starts after the first chunk, as the reference's per-stripe
+    EncodedReader does (segmentupload/encode.go:39-75).  With hash_pieces the
+    piece hashes need whole pieces, so that form encodes the segment in one
+    call before any reader returns."""
 
-    def __init__(self, segment, redundancy, hash_pieces: bool = False):
+    def __init__(self, segment, redundancy, hash_pieces: bool = False, chunk_stripes: int = 0):
         self.segment = segment  # bytes-like, numpy array, or PinnedBackend
         self.redundancy = redundancy
         self.hash_pieces = hash_pieces  # also compute every piece's BLAKE3 in the same engine call
+        self.chunk_stripes = chunk_stripes  # streamed upload chunk (0: the library's growing chunks)
         self._mu = threading.Lock()
         self._padded: Optional[np.ndarray] = None
         self._parity: Optional[PinnedHost] = None
         self._hashes: Optional[np.ndarray] = None
+        self._upload = None  # ec_upload handle of the streamed encode
         self._bufs = []
         self.stripes = 0
 
@@ -194,8 +232,11 @@ class SegmentPieceReader:
                                                              self._hashes.ctypes.data, N.EC_FLAG_PARITY_ONLY)
                 _raise(None, rc)
             elif n > k:
-                rc = N.load().ec_encode_segments_host(ctx, padded.ptr, 1, stripes, parity.ptr, N.EC_FLAG_PARITY_ONLY)
+                h = ctypes.c_void_p()
+                rc = N.load().ec_upload_begin(ctx, padded.ptr, stripes, parity.ptr, N.EC_FLAG_PARITY_ONLY,
+                                              self.chunk_stripes, ctypes.byref(h))
                 _raise(None, rc)
+                self._upload = h
             self.stripes = stripes
             self._padded = padded.array[:stripes * stripe].reshape(stripes, k, ess)
             self._parity = parity.array[:(n - k) * stripes * ess].reshape(n - k, stripes * ess)
@@ -209,8 +250,22 @@ class SegmentPieceReader:
             raise InfectiousError(f"num must be less than {n}")
         self._prepare()
         if num < k:  # EncodeSingle of a data share is the share itself (rs.go:21-23)
-            return _PieceStream(np.ascontiguousarray(self._padded[:, num, :]).reshape(-1))
-        return _PieceStream(self._parity[num - k])
+            return _DataPieceStream(self._padded, num)
+        return _PieceStream(self._parity[num - k], self._wait if self._upload is not None else None)
+
+    def _wait(self, end: int):
+        """Block until bytes [0, end) of every parity piece are in host memory."""
+        ess = self.redundancy.erasure_share_size()
+        h = self._upload
+        if h is None:
+            raise EEStreamError("piece reader used after close")
+        _raise(None, N.load().ec_upload_wait(h, (end + ess - 1) // ess))
+
+    def ready_stripes(self) -> int:
+        """Leading stripes of every parity piece already in host memory (no wait)."""
+        if self._upload is None:
+            return self.stripes if self._padded is not None else 0
+        return int(N.load().ec_upload_ready(self._upload))
 
     def piece_hash(self, num: int) -> bytes:
         """BLAKE3-256 of piece num: what the piecestore upload of that piece
@@ -223,7 +278,19 @@ class SegmentPieceReader:
         return self._hashes[num].tobytes()
 
     def close(self):
-        for b in self._bufs:
-            pinned_pool.put(b)
-        self._bufs = []
-        self._padded = self._parity = self._hashes = None
+        rc = 0
+        with self._mu:
+            if self._upload is not None:  # the engine may still be writing the parity buffer
+                rc = N.load().ec_upload_end(self._upload)
+                self._upload = None
+            for b in self._bufs:
+                pinned_pool.put(b)
+            self._bufs = []
+            self._padded = self._parity = self._hashes = None
+        _raise(None, rc)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
