@@ -134,8 +134,12 @@ int ec_rebuild_segments_batched(const ec_ctx *ctx, int nshares, const int *nums,
  * computed and tested for zero inside the kernel, nothing stored) and, where
  * a column is not a codeword, corrected by Berlekamp-Welch.  Corrected
  * shares are written back into the caller's pieces, as infectious corrects
- * share.Data in place.  Returns when done (the check's outcome is read back):
- * EC_ERR_TOO_MANY_ERRORS / EC_ERR_NOT_ENOUGH_SHARES as Decode returns them. */
+ * share.Data in place.  The check and the rebuild are one pass over the shares
+ * (the rebuilt rows stored, the syndrome rows tested in the same kernel); a
+ * segment with errors is then corrected and rebuilt again on its own.  Returns
+ * when done (the check's outcome is read back), also when nshares == k:
+ * EC_ERR_TOO_MANY_ERRORS / EC_ERR_NOT_ENOUGH_SHARES as Decode returns them.
+ * Of more than 128 shares (n > 128), the first 128 in number order are used. */
 int ec_decode_segments(const ec_ctx *ctx, int nshares, const int *nums, uint8_t *const *pieces, size_t nstripes,
                        uint8_t *out, ec_stream stream);
 /* The same over nseg segments in one check and one rebuild launch (strides as

@@ -994,3 +994,54 @@ def test_encoder_queue_reused_across_streams(oracle):
     finally:
         torch.cuda.synchronize()
         L.ec_destroy(ctx)
+
+
+@pytest.mark.parametrize("body", ["jt", "sl"])
+def test_decode_segments_fused_pass_every_shape(oracle, body):
+    """The fused Decode launch: rebuilt data rows stored,
+    syndrome rows checked for zero, present data shares copied, all in one
+    pass over the shares -- under both bodies, for every data share present
+    (m = 0: copies and syndromes only), all of them missing (29 rows + the
+    syndromes), k+1 and k+n/4 shares, a row count needing several passes of
+    the jump-table kernel (29 + 40), and a corrupted piece that the check must
+    catch and the per-segment path correct."""
+    k, n, ess, stripes = 29, 80, 256, 400
+    sch = scheme(k, n, ess)
+    want = _native.EC_BODY_JUMP_TABLE if body == "jt" else _native.EC_BODY_STRAIGHT_LINE
+    assert sch._lib.ec_set_body(sch._ctx, want) == 0
+    rng = np.random.default_rng(4)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    d_pieces = torch.from_numpy(ref).cuda().reshape(1, n, -1)
+    sets = [list(range(0, k + 1)), list(range(0, k + 20)), list(range(n - k - 1, n)), list(range(n - k - 20, n)),
+            list(range(n - k - 40, n)), [int(x) for x in rng.permutation(n)[:k + 7]]]
+    for nums in sets:
+        assert np.array_equal(gpu_decode_segments(sch, d_pieces, nums, stripes), seg), nums[:3]
+        assert sch._lib.ec_last_body(sch._ctx) == want
+    recv = ref.copy()
+    nums = list(range(n - k - 8, n))
+    recv[nums[2]] ^= rng.integers(1, 256, stripes * ess, dtype=np.uint8)
+    d_bad = torch.from_numpy(recv).cuda().reshape(1, n, -1)
+    assert np.array_equal(gpu_decode_segments(sch, d_bad, nums, stripes), seg)
+    assert np.array_equal(d_bad.cpu().numpy()[0][nums[2]], ref[nums[2]])
+
+
+def test_decode_segments_wide_code_more_than_128_shares(oracle):
+    """Decode of a wide code given more than 128 shares uses the
+    first 128 in number order (a launch takes at most 128 inputs) instead of
+    failing: RS(100,200) from 150 shares, clean and with one corrupted piece
+    among the first 128."""
+    k, n, ess, stripes = 100, 200, 256, 24
+    sch = scheme(k, n, ess)
+    rng = np.random.default_rng(150)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    nums = [int(x) for x in rng.permutation(n)[:150]]
+    d_pieces = torch.from_numpy(ref).cuda().reshape(1, n, -1)
+    assert np.array_equal(gpu_decode_segments(sch, d_pieces, nums, stripes), seg)
+    recv = ref.copy()
+    bad = sorted(nums)[5]
+    recv[bad] ^= rng.integers(1, 256, stripes * ess, dtype=np.uint8)
+    d_bad = torch.from_numpy(recv).cuda().reshape(1, n, -1)
+    assert np.array_equal(gpu_decode_segments(sch, d_bad, nums, stripes), seg)
+    assert np.array_equal(d_bad.cpu().numpy()[0][bad], ref[bad])

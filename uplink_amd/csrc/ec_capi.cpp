@@ -1905,6 +1905,53 @@ static int syndrome_plan(ec_ctx *c, const std::vector<int> &nums, PlanPtr *out) 
     }, out, ns);
 }
 
+// Fused Decode plan over the sorted share set (nums, all nshares of them as
+// inputs): first the rows of Rebuild -- the data shares infectious' share
+// choice leaves missing, from the shares it chooses (choose_shares) -- then the
+// syndrome rows of syndrome_plan.  One launch reads every share once, stores
+// the rebuilt rows (the present data shares are copied through) and checks
+// the syndrome rows for zero; *nrebuild = the number of rebuilt rows.
+static int fused_decode_plan(ec_ctx *c, const std::vector<int> &nums, PlanPtr *out, std::vector<int> &missing_out) {
+    const int k = c->k, ns = (int)nums.size(), extra = ns - k;
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, ns, nums.data(), order, ids);
+    if (rc) return rc;
+    std::vector<int> key{-4};
+    key.insert(key.end(), nums.begin(), nums.end());
+    rc = cached_plan(c, key, [&](std::vector<uint8_t> &M, int &rows, std::vector<int> &missing) {
+        // Rebuild rows over the chosen shares (their positions in the sorted list: order)
+        std::vector<uint8_t> m((size_t)k * k, 0);
+        for (int i = 0; i < k; i++) {
+            if (ids[i] < k) m[(size_t)i * k + i] = 1;
+            else memcpy(&m[(size_t)i * k], &c->G[(size_t)ids[i] * k], k);
+        }
+        if (!gf_invert(m.data(), k)) return EC_ERR_SINGULAR;
+        for (int i = 0; i < k; i++)
+            if (ids[i] >= k) missing.push_back(i);
+        const int nreb = (int)missing.size();
+        // syndrome rows over the first k sorted shares
+        std::vector<uint8_t> b((size_t)k * k);
+        for (int i = 0; i < k; i++) memcpy(&b[(size_t)i * k], &c->G[(size_t)nums[i] * k], k);
+        if (!gf_invert(b.data(), k)) return EC_ERR_SINGULAR;
+        rows = nreb + extra;
+        M.assign((size_t)std::max(rows, 1) * ns, 0);
+        for (int r = 0; r < nreb; r++)
+            for (int i = 0; i < k; i++) M[(size_t)r * ns + order[i]] = m[(size_t)missing[r] * k + i];
+        for (int r = 0; r < extra; r++) {
+            uint8_t *row = &M[(size_t)(nreb + r) * ns];
+            for (int col = 0; col < k; col++) {
+                uint8_t acc = 0;
+                for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[k + r] * k + t], b[(size_t)t * k + col]);
+                row[col] = acc;
+            }
+            row[k + r] = 1;
+        }
+        return EC_OK;
+    }, out, ns);
+    if (rc == EC_OK) missing_out = (*out)->missing;
+    return rc;
+}
+
 int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in, uint8_t *const *pieces_in,
                                size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
                                uint8_t *out, ec_stream stream) {
@@ -1914,7 +1961,7 @@ int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in
     if (nshares < k) return EC_ERR_NOT_ENOUGH_SHARES;
     for (int i = 0; i < nshares; i++)
         if (nums_in[i] < 0 || nums_in[i] >= c->n) return EC_ERR_INVALID_SHARE;
-    if (k > kMaxOps || nshares > kMaxOps) return EC_ERR_UNSUPPORTED;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
     if (nstripes == 0 || nseg == 0) return EC_OK;
     if (!out) return EC_ERR_INVALID_ARG;
     DeviceGuard dg(c->device);
@@ -1923,6 +1970,10 @@ int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in
     std::vector<int> ord(nshares);
     for (int i = 0; i < nshares; i++) ord[i] = i;
     std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return nums_in[x] < nums_in[y]; });
+    // a launch takes at most kMaxOps inputs: of more shares (a wide code, n > 128), the first
+    // kMaxOps in number order are checked, corrected and rebuilt from (every data share present
+    // among them; the rest are neither read nor corrected)
+    nshares = std::min(nshares, kMaxOps);
     std::vector<int> nums(nshares);
     std::vector<uint8_t *> pcs(nshares);
     for (int i = 0; i < nshares; i++) {
@@ -1936,9 +1987,45 @@ int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in
     Workspace *w = nullptr;
     int rc = EC_OK;
     uint32_t nbad = bits ? 0u : 1u;  // no bit-sliced check: take the workspace path
+    std::vector<const uint8_t *> cp(pcs.begin(), pcs.end());
+    bool fused = false;
     if (extra > 0 && bits) {
-        // Correct, clean case: the syndrome rows over every column, checked for zero
-        // inside the kernel (nothing stored); then Rebuild, queued behind it
+        // Decode, clean case, in one pass over the shares: the rebuilt data rows
+        // stored, the syndrome rows checked for zero inside the kernel (a segment
+        // with errors is redone below, Correct then Rebuild, over this output)
+        PlanPtr plan;
+        std::vector<int> missing;
+        rc = fused_decode_plan(c, nums, &plan, missing);
+        if (rc == EC_OK && plan->rows <= kMaxOps) {
+            w = acquire_ws(c, 16);
+            if (!w->d_buf) { release_ws(c, w); return EC_ERR_DEVICE; }
+            RsArgs a{};
+            const uint8_t *base = pcs[0];
+            for (auto p : pcs) base = std::min<const uint8_t *>(base, p);
+            a.in_base = base;
+            a.out_base = out;
+            a.in_stripe_stride = ess;
+            a.out_stripe_stride = (int64_t)k * ess;
+            a.in_seg_stride = piece_seg_stride;
+            a.out_seg_stride = out_seg_stride;
+            for (int i = 0; i < nshares; i++) {
+                a.in_off[i] = pcs[i] - base;
+                a.copy_off[i] = nums[i] < k ? (int64_t)nums[i] * ess : -1;
+            }
+            a.zero_check = (uint32_t *)w->d_buf;
+            a.nstore = (int32_t)missing.size();
+            std::vector<int64_t> out_off(std::max(plan->rows, 1), 0);
+            for (size_t r = 0; r < missing.size(); r++) out_off[r] = (int64_t)missing[r] * ess;
+            fill_geometry(a, ess, (int64_t)nstripes, (int64_t)nseg);
+            if (hipMemsetAsync(w->d_buf, 0, 4, s) != hipSuccess) rc = EC_ERR_DEVICE;
+            if (!rc) rc = run_matmul(c, a, out_off.data(), *plan, (int64_t)nseg, true, s);
+            if (!rc && hipMemcpyAsync(&nbad, w->d_buf, 4, hipMemcpyDeviceToHost, s) != hipSuccess) rc = EC_ERR_DEVICE;
+            fused = true;
+        }
+    }
+    if (!rc && !fused && extra > 0 && bits) {
+        // (a share set whose fused plan has more than kMaxOps rows) the syndrome rows
+        // checked for zero inside the kernel (nothing stored); then Rebuild
         w = acquire_ws(c, 16);
         if (!w->d_buf) { release_ws(c, w); return EC_ERR_DEVICE; }
         PlanPtr plan;
@@ -1963,11 +2050,10 @@ int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in
         if (!rc) rc = run_matmul(c, a, out_off.data(), *plan, (int64_t)nseg, true, s);
         if (!rc && hipMemcpyAsync(&nbad, w->d_buf, 4, hipMemcpyDeviceToHost, s) != hipSuccess) rc = EC_ERR_DEVICE;
     }
-    std::vector<const uint8_t *> cp(pcs.begin(), pcs.end());
-    if (!rc)
+    if (!rc && !fused)
         rc = rebuild_device(c, nshares, nums.data(), cp.data(), ess, (int64_t)nstripes, (int64_t)nseg,
                             piece_seg_stride, out_seg_stride, out, s);
-    if (extra > 0 && !rc && hipStreamSynchronize(s) != hipSuccess) rc = EC_ERR_DEVICE;
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EC_ERR_DEVICE;  // returns when done (header)
     if (w) {  // (released before the error path takes a workspace of its own)
         if (rc) (void)hipStreamSynchronize(s);
         release_ws(c, w);

@@ -49,16 +49,16 @@ struct RsArgs {
     int64_t blocks_per_seg;   // ceil(chunks_per_seg / 64)
     int64_t total_blocks;     // blocks_per_seg * nseg
     uint32_t *queue;          // zero work counters of this launch, see kQueueDoneWord (null: static assignment)
-    // runtime-matrix kernel: when set, the computed rows are checked for zero
-    // instead of stored (syndrome rows of ec_decode_segments); each wave that
-    // finds a non-zero byte in a valid column adds 1 here
+    // runtime-matrix kernel: when set, the computed rows from nstore on are
+    // checked for zero instead of stored (syndrome rows of ec_decode_segments);
+    // each wave that finds a non-zero byte in a valid column adds 1 here
     uint32_t *zero_check;
     int32_t ess;              // erasure share size, multiple of 16 for the bit-sliced path
     int32_t cps;              // ess / 16 (16-byte chunks per share per stripe)
     int32_t nin;              // number of inputs (k)
     int32_t nout;             // number of computed rows
     int32_t coef_ld;          // leading dimension of coef (multiple of 16)
-    int32_t pad_;
+    int32_t nstore;           // with zero_check: rows below this are stored, the rest checked (fused Decode)
     // byte ranges every input read / output write of the launch must stay in
     // (set by the host from the geometry above; the checked build of the
     // library, UPLINK_EC_CHECKED, skips any access outside them and reports it)

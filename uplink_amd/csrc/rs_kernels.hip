@@ -124,17 +124,20 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 #pragma unroll
                 for (int p = 0; p < 8; p++) rows[o][p] = acc[o][p];
             if (a.zero_check) {
-                // syndrome rows: any set bit of a valid column is an error (zero is zero
-                // in the bit-sliced layout too; plane bits 0-3 of each byte are chunk A,
-                // bits 4-7 chunk B)
+                // rows below a.nstore are stored (a fused Decode's rebuilt data
+                // shares), the rest are syndrome rows: any set bit of a valid column
+                // is an error (zero is zero in the bit-sliced layout too; plane bits
+                // 0-3 of each byte are chunk A, bits 4-7 chunk B)
+                const int nst = a.nstore;
                 uint32_t any = 0;
 #pragma unroll
                 for (int o = 0; o < OPW; o++)
-                    if (o < cnt)
+                    if (o < cnt && rbase + o >= nst)
 #pragma unroll
                         for (int p = 0; p < 8; p++) any |= rows[o][p];
                 any &= (c.vA ? 0x0F0F0F0Fu : 0u) | (c.vB ? 0xF0F0F0F0u : 0u);
                 if (__ballot(any != 0) != 0 && lane == 0) atomicAdd(a.zero_check, 1u);
+                if (rbase < nst) store_rows<OPW, true>(a, seg, c, rbase, nst - rbase < cnt ? nst - rbase : cnt, rows);
             } else {
                 store_rows<OPW, true>(a, seg, c, rbase, cnt, rows);
             }
