@@ -7,7 +7,7 @@ encode and rebuild launch on the launch stream, and the parity-only encode
 timed the same way; median and min over rounds.  Every build's pieces and
 rebuilds are checked against the first build's.
 
-  python tools/exp/ab_lib.py LIB_A LIB_B ... [--rounds 6] [--pairs 8]
+  python tools/exp/ab_lib.py LIB_A LIB_B[@VAR=VALUE,...] ... [--rounds 6] [--pairs 8]
 """
 from __future__ import annotations
 
@@ -58,11 +58,23 @@ def main():
     ptrs_c = [(ctypes.c_void_p * K)(*[pieces.data_ptr() + j * PIECE for j in s]) for s in sets]
     builds = []
     ref = None
-    for p in args.libs:
+    for spec in args.libs:
+        # LIB[@VAR=VALUE,...]: environment set while the context is created (engine knobs read at ec_create)
+        p, _, envs = spec.partition("@")
+        saved = {}
+        for kv in filter(None, envs.split(",")):
+            var, _, val = kv.partition("=")
+            saved[var] = os.environ.get(var)
+            os.environ[var] = val
         L = load(p)
         ctx = ctypes.c_void_p()
         assert L.ec_create(K, N, ESS, ctypes.byref(ctx)) == 0
-        tag = os.path.basename(os.path.dirname(os.path.abspath(p)))
+        for var, val in saved.items():
+            if val is None:
+                os.environ.pop(var)
+            else:
+                os.environ[var] = val
+        tag = os.path.basename(os.path.dirname(os.path.abspath(p))) + (f"@{envs}" if envs else "")
         pieces.zero_()
         assert L.ec_encode_segments(ctx, segs.data_ptr(), B, NSTRIPES, pieces.data_ptr(), 0, sptr) == 0
         torch.cuda.synchronize()

@@ -14,7 +14,7 @@
 // that store everything are checked byte for byte against the plain body.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/exp/enc_diag.hip -o tools/exp/bin/enc_diag
-//   tools/exp/bin/enc_diag [rounds]
+//   tools/exp/bin/enc_diag [rounds] [mode mask: 1 random b2b, 2 random alternating, 4 const, 8 zeros]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,9 +42,9 @@ constexpr int K = 29, N = 80, R = N - K, ESS = 256, NC = 8, NL = 4, NSEG = 16;
 constexpr int64_t NSTRIPES = (64ll * 1024 * 1024 + 4 + K * ESS - 1) / (K * ESS);
 constexpr int64_t SPAD = NSTRIPES * K * ESS, PLEN = NSTRIPES * ESS;
 
-template <bool COPY, int DIAG>
-__global__ __launch_bounds__((NC + NL) * 64, 1) void enc_diag(const RsArgs a) {
-    enc::encode_body<K, N, NC, NL, COPY, DIAG>(a);
+template <bool COPY, int DIAG, int NCV = NC, int NLV = NL>
+__global__ __launch_bounds__((NCV + NLV) * 64, 1) void enc_diag(const RsArgs a) {
+    enc::encode_body<K, N, NCV, NLV, COPY, DIAG>(a);
 }
 
 __global__ void fill_rand(uint8_t *p, int64_t n16, uint32_t seed) {
@@ -66,9 +66,9 @@ struct Variant {
     void (*launch)(const RsArgs &, int, hipStream_t);
 };
 
-template <bool COPY, int DIAG>
+template <bool COPY, int DIAG, int NCV = NC, int NLV = NL>
 void launch(const RsArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((enc_diag<COPY, DIAG>), dim3(grid), dim3((NC + NL) * 64), 0, s, a);
+    hipLaunchKernelGGL((enc_diag<COPY, DIAG, NCV, NLV>), dim3(grid), dim3((NCV + NLV) * 64), 0, s, a);
 }
 
 static RsArgs make_args(const uint8_t *segs, uint8_t *out, bool copy, uint32_t *queue, uint64_t *diag) {
@@ -124,7 +124,7 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     constexpr int S = enc::kDiagStamp, NP = enc::kDiagNoParityStores, NCP = enc::kDiagNoCopyStores;
-    constexpr int NCB = enc::kDiagNoCombos, NR = enc::kDiagNoRowOps;
+    constexpr int NCB = enc::kDiagNoCombos, NR = enc::kDiagNoRowOps, HC = enc::kDiagHalfCombos;
     const Variant vars[] = {
         {"full", true, 0, launch<true, 0>},
         {"full stamp", true, S, launch<true, S>},
@@ -134,11 +134,19 @@ int main(int argc, char **argv) {
         {"full nocombo", true, S | NCB, launch<true, S | NCB>},
         {"full norowops", true, S | NR, launch<true, S | NR>},
         {"full norow+nost", true, S | NR | NP | NCP, launch<true, S | NR | NP | NCP>},
+        {"full halfcombo", true, S | HC, launch<true, S | HC>},
+        {"full 4c+4l", true, S, launch<true, S, 4, 4>},
+        {"full 6c+4l", true, S, launch<true, S, 6, 4>},
+        {"full 6c+6l", true, S, launch<true, S, 6, 6>},
+        {"full 8c+8l", true, S, launch<true, S, 8, 8>},
         {"parity", false, 0, launch<false, 0>},
         {"parity stamp", false, S, launch<false, S>},
         {"parity nopar", false, S | NP, launch<false, S | NP>},
         {"parity nocombo", false, S | NCB, launch<false, S | NCB>},
         {"parity norowops", false, S | NR, launch<false, S | NR>},
+        {"parity halfcombo", false, S | HC, launch<false, S | HC>},
+        {"parity 4c+4l", false, S, launch<false, S, 4, 4>},
+        {"parity 6c+4l", false, S, launch<false, S, 6, 4>},
     };
     const double alg_full = (double)SPAD * NSEG * (1.0 + (double)N / K);
     const double alg_par = (double)SPAD * NSEG * (1.0 + (double)R / K);
@@ -150,7 +158,9 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&cpy_b, SPAD * NSEG));
     std::vector<hipEvent_t> evs(40);
     for (auto &e : evs) CK(hipEventCreate(&e));
+    const int mode_mask = argc > 2 ? atoi(argv[2]) : 15;
     for (int mode = 0; mode < 4; mode++) {
+        if (!(mode_mask & (1 << mode))) continue;
         const bool alt = mode == 1;
         if (mode <= 1) hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, s, segs, SPAD * NSEG / 16, 12345u);
         else CK(hipMemsetAsync(segs, mode == 2 ? 0x5a : 0, SPAD * NSEG, s));

@@ -88,7 +88,8 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
             constexpr int M = M1 + 1;
             constexpr int low = M & (-M);
             constexpr int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
-            if constexpr (M == low || (DIAG & 8) != 0) {  // (kDiagNoCombos: every entry a single plane)
+            // (kDiagNoCombos: every entry a single plane; kDiagHalfCombos: so for the odd inputs)
+            if constexpr (M == low || (DIAG & 8) != 0 || ((DIAG & 32) != 0 && (J & 1) != 0)) {
                 lo[M] = x[bit];
                 hi[M] = x[4 + bit];
             } else {
@@ -156,7 +157,10 @@ __device__ __forceinline__ void wait_vm(int n) {
 //                         not built (every combination reads a single plane)
 //   kDiagNoRowOps         timing only: no multiply-add at all (the inputs' planes
 //                         are read from the LDS and kept live, the rows stay zero)
-constexpr int kDiagStamp = 1, kDiagNoParityStores = 2, kDiagNoCopyStores = 4, kDiagNoCombos = 8, kDiagNoRowOps = 16;
+//   kDiagHalfCombos       timing only: kDiagNoCombos for the odd inputs (what
+//                         building each input's combinations in half the waves saves)
+constexpr int kDiagStamp = 1, kDiagNoParityStores = 2, kDiagNoCopyStores = 4, kDiagNoCombos = 8, kDiagNoRowOps = 16,
+              kDiagHalfCombos = 32;
 
 __device__ __forceinline__ void sink16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     asm volatile("" ::"v"(x), "v"(y), "v"(z), "v"(w));
