@@ -1045,36 +1045,3 @@ def test_decode_segments_wide_code_more_than_128_shares(oracle):
     d_bad = torch.from_numpy(recv).cuda().reshape(1, n, -1)
     assert np.array_equal(gpu_decode_segments(sch, d_bad, nums, stripes), seg)
     assert np.array_equal(d_bad.cpu().numpy()[0][bad], ref[bad])
-
-
-@pytest.mark.parametrize("ring", ["1", "0"])
-def test_rebuild_ring_pipeline_vs_oracle(oracle, monkeypatch, ring):
-    """Whole-segment launches of straight-line plans with <= 32 rows and <= 31
-    inputs run in the encoder's ring pipeline (rs_rebuild_ring; UPLINK_EC_RING=0
-    keeps them on rs_matmul_jt): every count of missing data shares of
-    RS(29,80) (1 .. 29 rows: 2, 3 and 4 row groups), RS(20,60) ess 4096,
-    a single stripe and a ragged last tile, batched segments with strides, and
-    encodes on a parity plan's code (RS(20,50), 30 parity rows); every result
-    against the oracle, in both forms."""
-    monkeypatch.setenv("UPLINK_EC_RING", ring)
-    for (k, n, ess, stripes, nseg) in ((29, 80, 256, 700, 3), (20, 60, 4096, 37, 2), (29, 80, 256, 1, 1),
-                                       (7, 12, 512, 257, 2)):
-        sch = scheme(k, n, ess)
-        assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0
-        rng = np.random.default_rng(k + stripes)
-        segs = rng.integers(0, 256, (nseg, stripes * k * ess), dtype=np.uint8)
-        f = oracle.FEC(k, n)
-        refs = np.stack([f.encode_segment(s, ess, threads=8) for s in segs])
-        d_pieces = torch.from_numpy(refs).cuda()
-        for m in sorted({1, 2, 8, 16, 17, 24, 25, min(k, n - k)}):
-            if m > min(k, n - k):
-                continue
-            missing = sorted(rng.choice(k, m, replace=False).tolist())
-            nums = [j for j in range(k) if j not in missing] + sorted(rng.choice(np.arange(k, n), m, replace=False).tolist())
-            got = gpu_rebuild(sch, d_pieces, nums, stripes, nseg=nseg)
-            assert np.array_equal(got, segs), (k, n, m)
-            assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
-    sch = scheme(20, 50, 256)
-    seg = np.random.default_rng(5).integers(0, 256, 300 * 20 * 256, dtype=np.uint8)
-    ref = oracle.FEC(20, 50).encode_segment(seg, 256, threads=8)
-    assert np.array_equal(gpu_encode(sch, seg).cpu().numpy()[0], ref)

@@ -96,7 +96,7 @@ struct DevArena {
 
 struct MatPlan {
     std::shared_ptr<DevArena> arena;  // where d_coef, d_tgt and d_sl live
-    size_t coef_bytes = 0;
+    size_t coef_bytes = 0, sl_bytes = 0;
     std::vector<size_t> tgt_bytes;
     std::atomic<int> launches{0};     // launches made with this plan (straight-line code from the second on)
     std::vector<int> key;          // what the matrix is (decode: chosen share ids; see plan keys below)
@@ -106,14 +106,9 @@ struct MatPlan {
     std::vector<uint64_t *> d_tgt; // leaf addresses per block of kMaxOps rows
     std::vector<uint8_t> M;        // rows x nin, row-major (for the straight-line code)
     std::mutex sl_mu;
-    // the plan's straight-line code, made on demand per row split: [0] the
-    // runtime-matrix kernel's (sl::split_for), [1] the ring rebuild's (sl::ring_split)
-    struct SlCode {
-        bool tried = false;
-        hipModule_t mod = nullptr;
-        uint64_t *d = nullptr;     // segment addresses [pass][chunk][group]
-        size_t bytes = 0;
-    } sl[2];
+    bool sl_tried = false;
+    hipModule_t sl_mod = nullptr;
+    uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
     // Completion of the plan's launches: one event per caller stream, recorded
     // behind the stream's latest launch of this plan (note_use).  Teardown
     // waits on these alone -- a launch that used the plan may still be in
@@ -148,10 +143,9 @@ struct MatPlan {
         if (arena) {
             arena->release(d_coef, coef_bytes);
             for (size_t i = 0; i < d_tgt.size(); i++) arena->release((uint8_t *)d_tgt[i], tgt_bytes[i]);
-            for (auto &x : sl) arena->release((uint8_t *)x.d, x.bytes);
+            arena->release((uint8_t *)d_sl, sl_bytes);
         }
-        for (auto &x : sl)
-            if (x.mod) (void)hipModuleUnload(x.mod);
+        if (sl_mod) (void)hipModuleUnload(sl_mod);
     }
 };
 using PlanPtr = std::shared_ptr<MatPlan>;
@@ -264,10 +258,6 @@ struct ec_ctx {
     // at ec_create): EncodeSingle batches of more than M requests find no
     // staging, nor does a one-request batch for share J
     int fault_max_batch = 0, fault_fail_num = -1;
-    // whole-segment launches of a straight-line plan with <= 32 rows and <= 31
-    // inputs run in the ring pipeline (rs_rebuild_ring); UPLINK_EC_RING=0 at
-    // ec_create keeps them on rs_matmul_jt (A/B measurements; identical results)
-    bool ring = true;
 };
 
 namespace {
@@ -585,19 +575,16 @@ bool sl_encoder(const ec_ctx *c) {
            (c->body == EC_BODY_STRAIGHT_LINE || (c->body == EC_BODY_AUTO && c->n - c->k <= kSlEncodeMaxRows));
 }
 
-// Make the plan's straight-line module for one row split (once; on failure
-// the plan keeps using the jump table).  Synchronous, on the context's setup
-// stream.  which: 0 = rs_matmul_jt's split, 1 = the ring rebuild's.
-void ensure_sl(ec_ctx *c, MatPlan &plan, int which) {
+// Make the plan's straight-line module (once; on failure the plan keeps
+// using the jump table).  Synchronous, on the context's setup stream.
+void ensure_sl(ec_ctx *c, MatPlan &plan) {
     std::lock_guard<std::mutex> g(plan.sl_mu);
-    MatPlan::SlCode &x = plan.sl[which];
-    if (x.tried) return;
-    x.tried = true;
+    if (plan.sl_tried) return;
+    plan.sl_tried = true;
     if (plan.rows < 1 || plan.rows > kMaxOps || plan.nin < 1 || plan.nin > kMaxOps) return;
     std::vector<uint32_t> code(sl::kRegionWords, 0xbf810000u);  // s_endpgm
     std::vector<uint32_t> offs;
-    const sl::Split sp = which ? sl::ring_split(plan.rows) : sl::split_for(plan.rows);
-    const size_t used = sl::generate(plan.M.data(), plan.rows, plan.nin, sp, code.data(), code.size(), offs);
+    const size_t used = sl::generate(plan.M.data(), plan.rows, plan.nin, code.data(), code.size(), offs);
     if (!used) return;  // does not fit
     size_t roff = 0, rwords = 0;
     std::vector<uint8_t> img = sl::template_image(used, &roff, &rwords);
@@ -627,9 +614,9 @@ void ensure_sl(ec_ctx *c, MatPlan &plan, int which) {
     e = hipMemcpyAsync(d, tab.data(), tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, c->setup);
     if (e == hipSuccess) e = hipStreamSynchronize(c->setup);
     if (e != hipSuccess) return fail(e);
-    x.mod = mod;
-    x.d = d;
-    x.bytes = dbytes;
+    plan.sl_mod = mod;
+    plan.d_sl = d;
+    plan.sl_bytes = dbytes;
 }
 
 // Launch the product described by `a` with the rows of `plan` (out_off gives
@@ -645,6 +632,7 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64
         a.nin = plan.nin;
         a.coef = plan.d_coef + done;
         a.coef_ld = plan.coef_ld;
+        a.jt_tgt = bitsliced ? plan.d_tgt[blk] : nullptr;
         for (int r = 0; r < rows; r++) a.out_off[r] = out_off[done + r];
         if (done > 0)
             for (int j = 0; j < a.nin; j++) a.copy_off[j] = -1;
@@ -656,25 +644,12 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64
         const bool want_sl = bitsliced && total_rows <= kMaxOps && c->body != EC_BODY_JUMP_TABLE &&
                              (c->body == EC_BODY_STRAIGHT_LINE ||
                               (a.total_tiles >= kSlMinTiles && plan.launches.load() > 0));
-        // the encoder's ring pipeline with the plan's code (rs_rebuild_ring) where it fits
-        a.jt_tgt = nullptr;
-        const bool ring = want_sl && c->ring && a.nin <= kRingMaxInputs && rows <= kRingMaxRows && !a.zero_check;
-        if (ring) ensure_sl(c, plan, 1);
-        if (ring && plan.sl[1].d) {
-            a.jt_tgt = plan.sl[1].d;
-            c->last_body = EC_BODY_STRAIGHT_LINE;
-            int slot = -1;
-            a.queue = queue_take(c, s, &slot);
-            const hipError_t e = launch_rebuild_ring(a, s);
-            if (slot >= 0) queue_done(c, s, slot, e == hipSuccess);
-            a.queue = nullptr;
-            HIP_TRY(e);
-        } else if (want_sl && (ensure_sl(c, plan, 0), plan.sl[0].d)) {
-            a.jt_tgt = plan.sl[0].d;
+        if (want_sl) ensure_sl(c, plan);
+        if (want_sl && plan.d_sl) {
+            a.jt_tgt = plan.d_sl;
             c->last_body = EC_BODY_STRAIGHT_LINE;
             HIP_TRY(launch_matmul_sl(a, 0, s));
         } else if (bitsliced) {
-            a.jt_tgt = plan.d_tgt[blk];
             c->last_body = EC_BODY_JUMP_TABLE;
             HIP_TRY(launch_matmul_generic(a, 0, s));
         } else {
@@ -828,7 +803,6 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     HIP_TRY(hipMalloc(&c->d_chk, 4));
     HIP_TRY(hipMemset(c->d_chk, 0, 4));
 #endif
-    if (const char *r = getenv("UPLINK_EC_RING")) c->ring = atoi(r) != 0;
     if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
         if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;
     *out = c.release();

@@ -41,7 +41,6 @@
 
 #include "gf256_field.hpp"
 #include "rs_device.hpp"
-#include "rs_encoder.hpp"
 #include "rs_kernels.hpp"
 #include "rs_sl.hpp"
 
@@ -183,138 +182,6 @@ __global__ __launch_bounds__(NW * 64) void rs_copy_shares(const RsArgs a) {
                     if (c.vA && in_range(a, p + c.outA, true, 7)) st16<true>(p + c.outA, A[i].x, A[i].y, A[i].z, A[i].w);
                     if (c.vB && in_range(a, p + c.outB, true, 7)) st16<true>(p + c.outB, B[i].x, B[i].y, B[i].z, B[i].w);
                 }
-            }
-        }
-    }
-}
-
-// Rebuild of whole segments in the encoder's pipeline (rs_encoder.hpp), with
-// the decode plan's straight-line code as the multiply: one workgroup per CU
-// takes tiles (two 1-KiB column blocks of every input, pair_cols) from the
-// launch's queue; NL loader waves LDS-DMA all inputs of tile i+1 into one
-// slot of a 2-slot ring, bit-slice them in place and copy the present data
-// shares through to the segment, while NC compute waves run the plan's
-// segments over tile i in the other slot and store the rebuilt rows.  One
-// LDS-only barrier per tile.  The plan's code is generated for the ring's
-// split (rs_sl.hpp ring_split: one pass, the rows dealt to NC = kRingGroups
-// groups, two compute waves per SIMD), so compute wave g runs row group g over
-// every chunk of the plan, which here are consecutive inputs of the resident
-// slot.  At most kRingMaxInputs inputs (the generated code addresses input jj
-// of a chunk at 2048 jj within a 16-bit offset) and 8 rows per wave.
-constexpr int kRingMaxIn = kRingMaxInputs;
-
-template <int NC, int NL>
-__global__ __launch_bounds__((NC + NL) * 64, 1) void rs_rebuild_ring(const RsArgs a) {
-    constexpr int PERMAX = (kRingMaxIn + NL - 1) / NL;
-    __shared__ __attribute__((aligned(16))) u32x4 ring[2 * kRingMaxIn * 128];
-    __shared__ int32_t s_q[8];  // tile of the m-th take, at m & 7
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool loader = wave >= NC;
-    const int lw = wave - NC;
-    const bool taker = wave == 0 && lane == 0;
-    const int nin = a.nin, rows = a.nout;
-    const int slot_words = nin * 128;  // u32x4 per slot
-    const int64_t P = pair_count(a);
-    const uint32_t ring_addr = (uint32_t)(uint64_t)ring;
-    // the plan's split (rs_sl.hpp ring_split / generate): one pass, NC groups
-    constexpr int nw = NC;
-    const int jc = 2 * nw, nchunks = (nin + jc - 1) / jc, ch_size = (nin + nchunks - 1) / nchunks;
-    constexpr int K0 = 2;  // tiles taken before the loop (items 0 and 1)
-    auto tile_of = [&](int item) -> int64_t { return s_q[item & 7]; };
-    auto issue = [&](int sl, int64_t t) {
-        const TileCols c = pair_cols(a, t, lane);
-#pragma unroll
-        for (int i = 0; i < PERMAX; i++) {
-            const int j = lw + NL * i;
-            if (j < nin) {
-                const uint8_t *p = a.in_base + a.in_off[j];
-                const uint8_t *pa = p + (c.vA ? c.inA : 0), *pb = p + (c.vB ? c.inB : 0);
-                if (!in_range(a, pa, false, 8)) pa = a.chk_in_lo;
-                if (!in_range(a, pb, false, 8)) pb = a.chk_in_lo;
-                const uint32_t d = __builtin_amdgcn_readfirstlane(ring_addr + (uint32_t)(sl * slot_words * 16 + j * 2048));
-                dma_1k(pa, d);
-                dma_1k(pb, d + 1024);
-            }
-        }
-    };
-    auto slice = [&](int sl, int64_t t) {
-        const TileCols c = pair_cols(a, t, lane);
-        u32x4 *slot = ring + sl * slot_words;
-#pragma unroll
-        for (int i = 0; i < PERMAX; i++) {
-            const int j = lw + NL * i;
-            if (j < nin) {
-                const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
-                const int64_t co = a.copy_off[j];
-                if (co >= 0) {
-                    uint8_t *p = a.out_base + co;
-                    if (c.vA && in_range(a, p + c.outA, true, 9)) st16<true>(p + c.outA, A4.x, A4.y, A4.z, A4.w);
-                    if (c.vB && in_range(a, p + c.outB, true, 9)) st16<true>(p + c.outB, B4.x, B4.y, B4.z, B4.w);
-                }
-                uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
-                bitslice8(w);
-                slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
-                slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
-            }
-        }
-    };
-    if (taker)
-#pragma unroll
-        for (int m = 0; m < K0; m++) s_q[m] = enc::take_tile(a, m);
-    lds_barrier();
-    if (loader) {
-        const int64_t t0 = tile_of(0);
-        if (t0 < P) {
-            issue(0, t0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            slice(0, t0);
-        }
-    }
-    lds_barrier();
-    if (loader) {
-        for (int i = 0;; i++) {
-            if (tile_of(i) >= P) break;
-            const int64_t u1 = tile_of(i + 1);
-            if (u1 < P) {
-                issue((i + 1) & 1, u1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile i+1 landed (and tile i's copies left)
-                slice((i + 1) & 1, u1);
-            }
-            lds_barrier();
-        }
-    } else {
-        const int g = wave;
-        const int rbase = g * rows / nw, cnt = (g + 1) * rows / nw - rbase;
-        for (int m = 0;; m++) {
-            const int64_t ti = tile_of(m);
-            if (ti >= P) break;
-            // the tile two items on: its queue atomic returns during this item, published before the barrier
-            int32_t pending = 0;
-            if (taker && m + 2 >= K0) pending = enc::take_tile(a, m + 2);
-            if (cnt > 0) {
-                u32x8 acc[8];
-#pragma unroll
-                for (int o = 0; o < 8; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
-                const uint32_t xa = ring_addr + (uint32_t)((m & 1) * slot_words * 16) + (uint32_t)lane * 16;
-                for (int ch = 0; ch < nchunks; ch++)
-                    sl_segment(acc, xa + (uint32_t)(ch * ch_size * 2048), a.jt_tgt + ch * nw + g);
-                uint32_t rr[8][8];
-#pragma unroll
-                for (int o = 0; o < 8; o++)
-#pragma unroll
-                    for (int p = 0; p < 8; p++) rr[o][p] = acc[o][p];
-                const TileCols c = pair_cols(a, ti, lane);
-                store_rows<8, true>(a, 0, c, rbase, cnt, rr);
-            }
-            if (taker) s_q[(m + 2) & 7] = pending;
-            lds_barrier();
-        }
-        // the launch's last workgroup zeroes the queue (rs_encoder.hpp)
-        if (taker && a.queue) {
-            if (atomicAdd(a.queue + kQueueDoneWord, 1u) == gridDim.x - 1) {
-                atomicExch(a.queue, 0u);
-                atomicExch(a.queue + kQueueDoneWord, 0u);
             }
         }
     }
@@ -475,15 +342,6 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     default:
         hipLaunchKernelGGL((rs_matmul_jt<4, SL>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
     }
-    return hipGetLastError();
-}
-
-hipError_t launch_rebuild_ring(const RsArgs &a, hipStream_t s) {
-    if (a.nin < 1 || a.nin > kRingMaxInputs || a.nout < 1 || a.nout > kRingMaxRows || a.zero_check || !a.jt_tgt)
-        return hipErrorInvalidValue;
-    static_assert(kRingMaxRows == sl::kRingGroups * kJtRows, "one pass of 8 rows per compute wave");
-    const int grid = default_grid((a.total_blocks + 1) / 2, 1);
-    hipLaunchKernelGGL((rs_rebuild_ring<sl::kRingGroups, 4>), dim3(grid), dim3((sl::kRingGroups + 4) * 64), 0, s, a);
     return hipGetLastError();
 }
 

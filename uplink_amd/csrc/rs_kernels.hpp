@@ -45,13 +45,6 @@ hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t strea
 // The same kernel calling a plan's straight-line segments (rs_sl.hpp):
 // args.jt_tgt = their absolute addresses, [pass][chunk][group].
 hipError_t launch_matmul_sl(const RsArgs &args, int grid, hipStream_t stream);
-// Rebuild of whole segments in the encoder's ring pipeline (rs_rebuild_ring,
-// rs_kernels.hip) with a plan's straight-line segments for sl::ring_split in
-// args.jt_tgt: at most kRingMaxInputs inputs and kRingMaxRows rows, no
-// zero_check; args.queue a zero work counter pair (or null: tiles assigned
-// statically).
-constexpr int kRingMaxInputs = 31, kRingMaxRows = 64;
-hipError_t launch_rebuild_ring(const RsArgs &args, hipStream_t stream);
 size_t jt_targets_bytes(const RsArgs &args);
 hipError_t launch_jt_targets(const RsArgs &args, uint64_t *targets, hipStream_t stream);
 // Byte-wise fallback (any ess, any alignment); coef as above.

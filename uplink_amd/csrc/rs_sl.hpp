@@ -58,10 +58,6 @@ struct Split {
     int count(int pass, int g, int rows) const;
 };
 Split split_for(int rows);  // the kernel launch (launch_matmul_sl) uses the same split
-// The ring rebuild's split (rs_kernels.hip rs_rebuild_ring): one pass, the rows
-// dealt to kRingGroups groups (one per compute wave), rows <= 8 * kRingGroups.
-constexpr int kRingGroups = 8;
-Split ring_split(int rows);
 
 // Generate the segments of M (rows x nin, row-major) into `code` (cap words,
 // pre-filled by the caller).  seg_off receives, for [pass][chunk][group], the
@@ -70,9 +66,6 @@ Split ring_split(int rows);
 // does not fit in cap words.  Any plan of up to 128 rows and 128 inputs fits
 // kRegionWords.
 size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, size_t cap, std::vector<uint32_t> &seg_off);
-// the same for a given split (chunks of at most 2 * sp.nw inputs)
-size_t generate(const uint8_t *M, int rows, int nin, const Split &sp, uint32_t *code, size_t cap,
-                std::vector<uint32_t> &seg_off);
 
 // The template code object (an ELF) with room for `words` words of code
 // (the small template if they fit it, else the large one), its region

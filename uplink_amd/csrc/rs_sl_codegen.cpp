@@ -143,19 +143,8 @@ Split split_for(int rows) {
     return s;
 }
 
-Split ring_split(int rows) {
-    Split s;
-    s.nw = kRingGroups;
-    s.npass = 1;
-    return s;
-}
-
 size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, size_t cap, std::vector<uint32_t> &seg_off) {
-    return generate(M, rows, nin, split_for(rows), code, cap, seg_off);
-}
-
-size_t generate(const uint8_t *M, int rows, int nin, const Split &sp, uint32_t *code, size_t cap,
-                std::vector<uint32_t> &seg_off) {
+    const Split sp = split_for(rows);
     const int jc = 2 * sp.nw, nchunks = (nin + jc - 1) / jc, ch_size = (nin + nchunks - 1) / nchunks;
     seg_off.assign((size_t)sp.npass * nchunks * sp.nw, kNoSegment);
     Emitter e{code, cap};
