@@ -138,6 +138,27 @@ def test_put_error_after_cut_counts_as_canceled(cpu_rs):
     assert nodes[2] is None and nodes[6] is None
 
 
+def test_put_canceled_by_user(cpu_rs):
+    """client.go:232-243 tells a user cancel (the parent context)
+    from the long-tail cut: with the caller's context canceled while uploads
+    are in flight, every upload still running fails as "upload canceled by
+    user" with context.Canceled first in the chain, and put fails below the
+    repair threshold."""
+    import threading
+    rng = np.random.default_rng(12)
+    lim = limits_for(10, 12)
+    store = _BrokenOnCancelStore(delay={l.node_id: 5.0 for l in lim})
+    c = ecclient.ECClient(store)
+    parent = threading.Event()
+    threading.Timer(0.2, parent.set).start()
+    with pytest.raises(ecclient.ECClientError) as ei:
+        c.put(lim, cpu_rs, io.BytesIO(rng.bytes(20_000)), parent=parent)
+    msg = str(ei.value)
+    assert "successful puts (0) less than or equal to repair threshold" in msg
+    assert "upload canceled by user: connection reset by peer" in msg and "slow connection" not in msg
+    assert c.last_counts["canceled"] == 10 and c.last_counts["failed"] == 0
+
+
 def test_put_single_result_cpu(cpu_rs):
     c = ecclient.ECClient(ecclient.LoopbackPieceStore())
     res = c.put_single_result(limits_for(10, 3), cpu_rs, io.BytesIO(b"hello" * 999))

@@ -160,9 +160,12 @@ class ECClient:
         return self
 
     # ------------------------------------------------------------- upload
-    def put_piece(self, limit: Optional[AddressedOrderLimit], reader, cancel: threading.Event):
+    def put_piece(self, limit: Optional[AddressedOrderLimit], reader, cancel: threading.Event,
+                  parent: Optional[threading.Event] = None):
         """PutPiece (client.go:211-256): a nil limit drains its reader; the
-        store's error is wrapped like the reference wraps the upload error."""
+        store's error is wrapped like the reference wraps the upload error.
+        `cancel` is the pieces context (canceled by the long-tail cut or with
+        its parent), `parent` the caller's context."""
         try:
             if limit is None:
                 streams.read_all(reader)
@@ -170,20 +173,26 @@ class ECClient:
             try:
                 return self.store.put_piece(limit, reader, cancel)
             except Exception as e:  # noqa: BLE001 - the reference wraps every upload error
-                if cancel.is_set():
+                user = parent is not None and parent.is_set()
+                if cancel.is_set() or user:
                     # client.go:232-243: once the pieces context is canceled, whatever the store
-                    # returned is a cancel, with context.Canceled the primary error of the chain
-                    raise ECClientError(f"upload cut due to slow connection (node:{limit.node_id.hex()}): {e}",
-                                        e if isinstance(e, Canceled) else Canceled(f"context canceled: {e}"))
+                    # returned is a cancel -- by the user when the parent context is canceled, else
+                    # the long-tail cut -- with context.Canceled the primary error of the chain
+                    cause = e if isinstance(e, Canceled) else Canceled(f"context canceled: {e}")
+                    if user:
+                        raise ECClientError(f"upload canceled by user: {e}", cause)
+                    raise ECClientError(f"upload cut due to slow connection (node:{limit.node_id.hex()}): {e}", cause)
                 raise ECClientError(f"upload failed (node:{limit.node_id.hex()}, address:{limit.address}): {e}", e)
         finally:
             if hasattr(reader, "close"):
                 reader.close()
 
     def put(self, limits: List[Optional[AddressedOrderLimit]], rs: eestream.RedundancyStrategy,
-            data) -> Tuple[List[Optional[dict]], List[object]]:
+            data, parent: Optional[threading.Event] = None) -> Tuple[List[Optional[dict]], List[object]]:
         """put (client.go:103-209): returns (successful nodes, hashes) indexed
-        by piece number, None where a piece was not stored."""
+        by piece number, None where a piece was not stored.  `parent` is the
+        caller's context: setting it cancels every upload in flight, which
+        then fail as "upload canceled by user"."""
         piece_count = len(limits)
         if piece_count != rs.total_count():
             raise ECClientError(f"size of limits slice ({piece_count}) does not match total count "
@@ -202,9 +211,18 @@ class ECClient:
         infos: List[Tuple[int, Optional[BaseException], object]] = []
         cv = threading.Condition()
 
+        done = threading.Event()
+        if parent is not None:
+            def watch():  # piecesCtx is a child of the caller's context (client.go:139)
+                while not done.is_set():
+                    if parent.wait(0.02):
+                        cancel.set()
+                        return
+            threading.Thread(target=watch, daemon=True).start()
+
         def one(i: int):
             try:
-                h = self.put_piece(limits[i], readers[i], cancel)
+                h = self.put_piece(limits[i], readers[i], cancel, parent)
                 res = (i, None, h)
             except BaseException as e:  # noqa: BLE001 - collected like the info channel
                 res = (i, e, None)
@@ -240,6 +258,7 @@ class ECClient:
                 cancel.set()  # cancelling remaining uploads (:178-181)
         for t in threads:
             t.join()
+        done.set()
         self.last_counts = {"total": piece_count, "optimal": rs.optimal_threshold(), "successful": successful,
                             "failed": failed, "canceled": canceled}
         joined = "; ".join(str(e) for e in errors)
