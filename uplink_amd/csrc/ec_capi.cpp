@@ -215,17 +215,23 @@ struct UploadSlot {
 // ring is made.  The last workgroup of a launch puts its pair back to zero
 // (rs_encoder.hpp), so a launch needs no memset before it.  A slot serves one
 // launch at a time: it goes to a launch on the stream its previous launch ran
-// on (stream order), or to any stream once the event behind its previous
-// launch has completed; with no such slot the launch assigns its tiles
-// statically (identical results).  No launch waits on another stream.
+// on (stream order), or to another stream once an event recorded right behind
+// its previous launch has completed; with no such slot the launch assigns its
+// tiles statically (identical results).  No launch waits on another stream.
+// The event is recorded behind every kEventEvery-th launch of a slot only (a
+// marker on the stream costs a few microseconds per launch): a slot whose
+// latest launch has none is reused by its own stream alone.
 struct QueueRing {
     static constexpr int kSlots = 32;
     static constexpr int kStride = 64;  // words per slot: the counter pair (kQueueDoneWord), a slot per 256 bytes
     std::mutex mu;
     uint32_t *d = nullptr;
+    int event_every = 8;                // UPLINK_EC_QUEUE_EVENT_EVERY at ec_create (A/B measurements)
     hipEvent_t ev[kSlots] = {};
-    hipStream_t owner[kSlots] = {};  // stream of the slot's last launch
+    hipStream_t owner[kSlots] = {};     // stream of the slot's last launch
     bool used[kSlots] = {}, busy[kSlots] = {};
+    bool covered[kSlots] = {};          // the event follows the slot's latest launch
+    int since[kSlots] = {};             // the slot's launches since its last event
 };
 
 struct ec_ctx {
@@ -538,7 +544,7 @@ uint32_t *queue_take(ec_ctx *c, hipStream_t s, int *slot) {
         if (q.used[i] && !q.busy[i] && q.owner[i] == s && q.ev[i]) pick = i;
     // else a fresh slot, or one whose last launch (on another stream) has completed
     for (int i = 0; i < QueueRing::kSlots && pick < 0; i++)
-        if (!q.busy[i] && q.ev[i] && (!q.used[i] || hipEventQuery(q.ev[i]) == hipSuccess)) pick = i;
+        if (!q.busy[i] && q.ev[i] && (!q.used[i] || (q.covered[i] && hipEventQuery(q.ev[i]) == hipSuccess))) pick = i;
     if (pick < 0) return nullptr;
     q.busy[pick] = true;
     *slot = pick;
@@ -549,9 +555,13 @@ void queue_done(ec_ctx *c, hipStream_t s, int slot, bool launched) {
     QueueRing &q = c->qring;
     std::lock_guard<std::mutex> g(q.mu);
     if (launched) {
-        q.used[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
-        if (!q.used[slot]) (void)hipStreamSynchronize(s);  // no event: let the launch finish before the slot returns
+        q.used[slot] = true;
         q.owner[slot] = s;
+        q.covered[slot] = false;
+        if (++q.since[slot] >= q.event_every) {
+            q.since[slot] = 0;
+            q.covered[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
+        }
     }
     q.busy[slot] = false;
 }
@@ -803,6 +813,7 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     HIP_TRY(hipMalloc(&c->d_chk, 4));
     HIP_TRY(hipMemset(c->d_chk, 0, 4));
 #endif
+    if (const char *e = getenv("UPLINK_EC_QUEUE_EVENT_EVERY")) c->qring.event_every = std::max(1, atoi(e));
     if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
         if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;
     *out = c.release();
@@ -836,6 +847,11 @@ void ec_destroy(ec_ctx *c) {
     c->enc_row.clear();
     if (c->setup) (void)hipStreamSynchronize(c->setup), (void)hipStreamDestroy(c->setup);
     if (c->d_chk) (void)hipFree(c->d_chk);
+    // a slot whose latest launch has no event behind it may still be in use on a
+    // caller's stream: then wait for the device before the counters are freed
+    bool uncovered = false;
+    for (int i = 0; i < QueueRing::kSlots; i++) uncovered = uncovered || (c->qring.used[i] && !c->qring.covered[i]);
+    if (uncovered) (void)hipDeviceSynchronize();
     for (int i = 0; i < QueueRing::kSlots; i++)
         if (c->qring.ev[i]) (void)hipEventSynchronize(c->qring.ev[i]), (void)hipEventDestroy(c->qring.ev[i]);
     if (c->qring.d) (void)hipFree(c->qring.d);

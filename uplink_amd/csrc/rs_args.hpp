@@ -65,10 +65,10 @@ struct RsArgs {
     const uint8_t *chk_in_lo, *chk_in_hi;
     const uint8_t *chk_out_lo, *chk_out_hi;
     uint32_t *chk_flag;       // checked build: first violating site (0 = none)
-    uint64_t *diag;           // diagnostic encoder forms only (rs_encoder.hpp kDiagStamp); null otherwise
     int64_t in_off[kMaxOps];  // bytes from in_base (16-byte aligned on the bit-sliced path)
     int64_t out_off[kMaxOps]; // bytes from out_base
     int64_t copy_off[kMaxOps];// bytes from out_base, -1 = no copy
+    uint64_t *diag;           // diagnostic encoder forms only (rs_encoder.hpp kDiagStamp); null otherwise
 };
 
 }  // namespace uplink_ec
