@@ -94,8 +94,62 @@ struct DevArena {
     }
 };
 
+// Completion marks of a context's runtime-matrix launches, per caller stream.
+// Each launch gets the next sequence number of its stream; an event is
+// recorded behind every kEvery-th launch only (a marker on the stream costs
+// microseconds per launch).  Launch q on stream s is known complete once an
+// event recorded at or after it has completed.  Events are recorded only at
+// launch time, on the stream being launched on, and queried afterwards (never
+// recorded on a stream the caller may have destroyed since).
+struct StreamMarks {
+    static constexpr int kEvery = 8;
+    static constexpr size_t kMaxStreams = 32;
+    struct Mark {
+        hipStream_t s = nullptr;
+        uint64_t issued = 0, ev_seq = 0;
+        int since = 0;
+        hipEvent_t ev = nullptr;
+    };
+    std::mutex mu;
+    std::deque<Mark> marks;  // most recently used streams last
+    // note a launch just queued on s; returns its sequence number (0: untracked)
+    uint64_t launched(hipStream_t s) {
+        std::lock_guard<std::mutex> g(mu);
+        Mark *m = nullptr;
+        for (auto &x : marks)
+            if (x.s == s) m = &x;
+        if (!m) {
+            if (marks.size() >= kMaxStreams) {  // the least recently used stream's marks go
+                if (marks.front().ev) (void)hipEventDestroy(marks.front().ev);
+                marks.pop_front();
+            }
+            marks.emplace_back();
+            m = &marks.back();
+            m->s = s;
+            if (hipEventCreateWithFlags(&m->ev, hipEventDisableTiming) != hipSuccess) m->ev = nullptr;
+        }
+        const uint64_t q = ++m->issued;
+        if (++m->since >= kEvery && m->ev && hipEventRecord(m->ev, s) == hipSuccess) {
+            m->since = 0;
+            m->ev_seq = q;
+        }
+        return q;
+    }
+    bool done(hipStream_t s, uint64_t q) {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto &x : marks)
+            if (x.s == s) return q != 0 && x.ev && x.ev_seq >= q && hipEventQuery(x.ev) == hipSuccess;
+        return false;
+    }
+    ~StreamMarks() {
+        for (auto &x : marks)
+            if (x.ev) (void)hipEventSynchronize(x.ev), (void)hipEventDestroy(x.ev);
+    }
+};
+
 struct MatPlan {
     std::shared_ptr<DevArena> arena;  // where d_coef, d_tgt and d_sl live
+    std::shared_ptr<StreamMarks> marks;  // the context's completion marks
     size_t coef_bytes = 0, sl_bytes = 0;
     std::vector<size_t> tgt_bytes;
     std::atomic<int> launches{0};     // launches made with this plan (straight-line code from the second on)
@@ -109,37 +163,31 @@ struct MatPlan {
     bool sl_tried = false;
     hipModule_t sl_mod = nullptr;
     uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
-    // Completion of the plan's launches: one event per caller stream, recorded
-    // behind the stream's latest launch of this plan (note_use).  Teardown
-    // waits on these alone -- a launch that used the plan may still be in
-    // flight when its last reference goes -- instead of synchronising the
-    // whole device (other contexts' and unrelated work included).
+    // The plan's launches, as (stream, sequence number) of the context's
+    // completion marks: the latest per stream.  A plan is destroyed only when
+    // every one of them is known complete (evicted plans wait in the context's
+    // graveyard for that); if not -- its last reference went elsewhere, or the
+    // marks were dropped -- the destructor synchronises the device instead.
     std::mutex use_mu;
-    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
-    static constexpr size_t kMaxUseStreams = 16;
+    std::vector<std::pair<hipStream_t, uint64_t>> uses;
     void note_use(hipStream_t s) {
+        const uint64_t q = marks ? marks->launched(s) : 0;
         std::lock_guard<std::mutex> g(use_mu);
         for (auto &u : uses)
             if (u.first == s) {
-                (void)hipEventRecord(u.second, s);
+                u.second = q;
                 return;
             }
-        hipEvent_t e = nullptr;
-        if (uses.size() >= kMaxUseStreams) {
-            // the oldest stream's entry: once its last launch of this plan is
-            // done it has nothing in flight here, and its event can be reused
-            e = uses.front().second;
-            (void)hipEventSynchronize(e);
-            uses.erase(uses.begin());
-        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-            (void)hipStreamSynchronize(s);  // no event: make this launch finish now instead
-            return;
-        }
-        (void)hipEventRecord(e, s);
-        uses.emplace_back(s, e);
+        uses.emplace_back(s, q);
+    }
+    bool idle() {
+        std::lock_guard<std::mutex> g(use_mu);
+        for (auto &u : uses)
+            if (!marks || !marks->done(u.first, u.second)) return false;
+        return true;
     }
     ~MatPlan() {
-        for (auto &u : uses) (void)hipEventSynchronize(u.second), (void)hipEventDestroy(u.second);
+        if (!uses.empty() && !idle()) (void)hipDeviceSynchronize();
         if (arena) {
             arena->release(d_coef, coef_bytes);
             for (size_t i = 0; i < d_tgt.size(); i++) arena->release((uint8_t *)d_tgt[i], tgt_bytes[i]);
@@ -244,6 +292,8 @@ struct ec_ctx {
     std::vector<uint8_t> G;        // n x k
     hipStream_t setup = nullptr;   // plan uploads (synchronous, never a caller's stream)
     std::shared_ptr<DevArena> arena = std::make_shared<DevArena>();
+    std::shared_ptr<StreamMarks> marks = std::make_shared<StreamMarks>();
+    std::vector<PlanPtr> graveyard;  // evicted plans whose launches may still run (under mu)
     std::mutex setup_mu;
     std::mutex mu;
     std::list<PlanPtr> plans;      // decode / re-encode plans, MRU first
@@ -394,6 +444,7 @@ void set_extents(RsArgs &a, int64_t nseg, uint32_t *chk) {
 int build_plan(ec_ctx *c, std::vector<int> key, const uint8_t *M, int rows, int nin, PlanPtr *out) {
     PlanPtr p = std::make_shared<MatPlan>();
     p->arena = c->arena;
+    p->marks = c->marks;
     p->key = std::move(key);
     p->rows = rows;
     p->nin = nin;
@@ -446,19 +497,33 @@ int cached_plan(ec_ctx *c, const std::vector<int> &key, F &&make_matrix, PlanPtr
     rc = build_plan(c, key, M.data(), rows, nin < 0 ? c->k : nin, &p);
     if (rc) return rc;
     p->missing = std::move(missing);
-    std::vector<PlanPtr> evicted;
+    std::vector<PlanPtr> reaped;
     {
         std::lock_guard<std::mutex> g(c->mu);
         c->plans.push_front(p);
+        // an evicted plan may still be read by launches in flight on callers'
+        // streams: it waits in the graveyard until its launches are known
+        // complete (MatPlan::idle, no wait); past kMaxPlans waiting, the device
+        // is synchronised once and all of them go
         while (c->plans.size() > kMaxPlans) {
-            evicted.push_back(c->plans.back());
+            c->graveyard.push_back(c->plans.back());
             c->plans.pop_back();
         }
+        for (auto it = c->graveyard.begin(); it != c->graveyard.end();) {
+            if ((*it)->idle()) {
+                reaped.push_back(*it);
+                it = c->graveyard.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        if (c->graveyard.size() > kMaxPlans) {
+            (void)hipDeviceSynchronize();
+            for (auto &x : c->graveyard) reaped.push_back(x);
+            c->graveyard.clear();
+        }
     }
-    // an evicted plan may still be read by launches in flight on callers'
-    // streams: its destructor (here, or wherever its last reference goes)
-    // waits for exactly those launches (MatPlan::note_use)
-    evicted.clear();
+    reaped.clear();  // (destroyed outside the lock)
     *out = p;
     return EC_OK;
 }
@@ -843,6 +908,7 @@ void ec_destroy(ec_ctx *c) {
         if (w->h_buf) (void)hipHostFree(w->h_buf);
     }
     c->plans.clear();
+    c->graveyard.clear();
     c->enc_parity.reset();
     c->enc_row.clear();
     if (c->setup) (void)hipStreamSynchronize(c->setup), (void)hipStreamDestroy(c->setup);
