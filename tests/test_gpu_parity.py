@@ -539,6 +539,44 @@ def test_rebuild_every_missing_count(oracle, k, n, body):
             assert sch._lib.ec_last_body(sch._ctx) == body
 
 
+@pytest.mark.parametrize("depth", [0, 2, 3])
+def test_rebuild_prefetch_depths_bit_exact(oracle, monkeypatch, depth):
+    """The straight-line rebuild's input pipeline (rs_matmul_dma: LDS-DMA of
+    the next chunk(s) of input shares, counted vmcnt waits, in-place slicing)
+    at every prefetch depth the library builds, and the register-staged kernel
+    (depth 0), against the segment: every missing count of RS(29,80) and
+    RS(50,80) (2-4 waves), a 2-segment batch with a ragged last tile, and an
+    RS(128,256) parity-heavy set (8 waves, two passes).  The depth is set at
+    ec_create and is library-wide, so the test ends by creating a context at
+    the default depth again."""
+    monkeypatch.setenv("UPLINK_EC_REBUILD_DEPTH", str(depth))
+    try:
+        for k, n, stripes, nseg in [(29, 80, 41, 2), (50, 80, 9, 1)]:
+            sch = scheme(k, n, 256)
+            assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0
+            rng = np.random.default_rng(depth * 100 + k)
+            seg = rng.integers(0, 256, nseg * stripes * k * 256, dtype=np.uint8)
+            d_pieces = gpu_encode(sch, seg, nseg=nseg)
+            for m in range(0, min(k, n - k) + 1):
+                nums = sorted(rng.choice(k, k - m, replace=False).tolist()) + \
+                    sorted(rng.choice(np.arange(k, n), m, replace=False).tolist())
+                got = gpu_rebuild(sch, d_pieces, nums, stripes, nseg=nseg)
+                assert np.array_equal(got.reshape(-1), seg), (k, m)
+        k, n, stripes = 128, 256, 3
+        sch = scheme(k, n, 256)
+        assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0
+        rng = np.random.default_rng(depth)
+        seg = rng.integers(0, 256, stripes * k * 256, dtype=np.uint8)
+        ref = oracle.FEC(k, n).encode_segment(seg, 256, threads=4)
+        d_pieces = torch.from_numpy(np.ascontiguousarray(ref)).cuda().reshape(1, n, -1)
+        nums = sorted(rng.choice(np.arange(k, n), 100, replace=False).tolist()) + list(range(28))
+        assert np.array_equal(gpu_rebuild(sch, d_pieces, sorted(nums), stripes)[0], seg)
+        assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
+    finally:
+        monkeypatch.delenv("UPLINK_EC_REBUILD_DEPTH")
+        scheme(29, 80, 256)  # back to the default depth
+
+
 @pytest.mark.parametrize("k,n,ess,stripes", [c for c in CONFIGS if c[2] % 16 == 0])
 def test_straight_line_body_vs_oracle(oracle, k, n, ess, stripes):
     """Every bit-sliced configuration with the straight-line body forced:

@@ -879,6 +879,7 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     HIP_TRY(hipMemset(c->d_chk, 0, 4));
 #endif
     if (const char *e = getenv("UPLINK_EC_QUEUE_EVENT_EVERY")) c->qring.event_every = std::max(1, atoi(e));
+    configure_rebuild(getenv("UPLINK_EC_REBUILD_DEPTH") ? atoi(getenv("UPLINK_EC_REBUILD_DEPTH")) : 1);
     if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
         if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;
     *out = c.release();

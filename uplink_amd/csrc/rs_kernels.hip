@@ -143,6 +143,143 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     }
 }
 
+// rs_matmul_jt's straight-line form with the input shares requested straight
+// into LDS (LDS-DMA, no registers held): the DMAs of chunk c+D are issued
+// after chunk c's barrier, so D chunks of every wave's loads are in flight
+// while it multiplies (rs_matmul_jt: one, in registers).  A ring of D+1 slots
+// of 2*NW inputs each; the issuing wave waits for its own DMAs by a counted
+// vmcnt and bit-slices them in place (the wide layout the straight-line
+// code reads), copying the present data shares through on the way.  Every
+// lane issues the copy-through stores (a lane past the end of the segment
+// rewrites column 0 with the bytes already there), so each wave's count of
+// VMEM operations is exact.  Each pass's pipeline starts and drains within
+// the pass.
+template <int NW, int D>
+__global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
+    constexpr int JC = 2 * NW, OPW = kJtRows, S = D + 1, SLOT = JC * 2048;
+    static_assert(D >= 1 && D <= 3, "store ring below holds at most 2 chunks");
+#ifdef UPLINK_EC_CHECKED
+    constexpr bool kCountStores = false;  // the checked build may skip a store: count none (waits longer)
+#else
+    constexpr bool kCountStores = true;
+#endif
+    const int nchunks = (a.nin + JC - 1) / JC;
+    const int CH = (a.nin + nchunks - 1) / nchunks;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    u32x4 *ring = (u32x4 *)smem;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = (wave + (int)(blockIdx.x % NW)) % NW;
+    const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
+    const uint32_t ring_addr = (uint32_t)(uintptr_t)smem;
+    // inputs of chunk ch this wave owns (j = wave, wave + NW; CH <= 2 NW)
+    auto owned = [&](int ch) -> int {
+        const int jn = a.nin - ch * CH < CH ? a.nin - ch * CH : CH;
+        return (wave < jn ? 1 : 0) + (wave + NW < jn ? 1 : 0);
+    };
+    for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
+        const int64_t seg = tile / a.tiles_per_seg;
+        const TileCols c = tile_cols(a, tile - seg * a.tiles_per_seg, lane);
+        const uint8_t *in_seg = a.in_base + seg * a.in_seg_stride;
+        uint8_t *out_seg = a.out_base + seg * a.out_seg_stride;
+        const int64_t iA = c.vA ? c.inA : 0, iB = c.vB ? c.inB : 0;
+        const int64_t oA = c.vA ? c.outA : 0, oB = c.vB ? c.outB : 0;
+        auto issue = [&](int ch) {
+            const uint32_t d0 = ring_addr + (uint32_t)((ch % S) * SLOT);
+            const int j0 = ch * CH;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int j = wave + NW * i;
+                if (i < owned(ch)) {
+                    const uint8_t *p = in_seg + a.in_off[j0 + j];
+                    const uint8_t *pa = p + iA, *pb = p + iB;
+                    if (!in_range(a, pa, false, 4)) pa = a.chk_in_lo;
+                    if (!in_range(a, pb, false, 4)) pb = a.chk_in_lo;
+                    const uint32_t d = __builtin_amdgcn_readfirstlane(d0 + (uint32_t)(j * 2048));
+                    dma_1k(pa, d);
+                    dma_1k(pb, d + 1024);
+                }
+            }
+        };
+        for (int pass = 0; pass < npass; pass++) {
+            const int p0 = pass * a.nout / npass, prow = (pass + 1) * a.nout / npass - p0;
+            const int rbase = p0 + group * prow / NW;
+            const int cnt = p0 + (group + 1) * prow / NW - rbase;
+            const bool do_copy = pass == 0;
+            u32x8 acc[OPW];
+#pragma unroll
+            for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
+            for (int y = 0; y < D && y < nchunks; y++) issue(y);
+            int st1 = 0, st2 = 0;  // copy-through stores of the last two slices (newest first)
+            for (int ch = 0; ch < nchunks; ch++) {
+                // this wave's VMEM operations issued after chunk ch's DMAs: the stores of
+                // slices ch-D+1 .. ch-1 and the DMAs of chunks ch+1 .. ch+D-1 (in order
+                // of completion, so waiting down to that many means chunk ch has landed)
+                int after = 0;
+                if constexpr (kCountStores) after += (D >= 2 ? st1 : 0) + (D >= 3 ? st2 : 0);
+#pragma unroll
+                for (int y = 1; y < D; y++)
+                    if (ch + y < nchunks) after += 2 * owned(ch + y);
+                wait_vm(after);
+                // bit-slice this wave's inputs of chunk ch in place
+                const int j0 = ch * CH;
+                u32x4 *slot = ring + (ch % S) * (SLOT / 16);
+                int st = 0;
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int j = wave + NW * i;
+                    if (i < owned(ch)) {
+                        const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
+                        const int64_t co = a.copy_off[j0 + j];
+                        if (do_copy && co >= 0) {
+                            uint8_t *p = out_seg + co;
+                            if (in_range(a, p + oA, true, 5)) st16<true>(p + oA, A4.x, A4.y, A4.z, A4.w);
+                            if (in_range(a, p + oB, true, 5)) st16<true>(p + oB, B4.x, B4.y, B4.z, B4.w);
+                            st += 2;
+                        }
+                        uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
+                        bitslice8(w);
+                        slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
+                        slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
+                    }
+                }
+                st2 = st1;
+                st1 = st;
+                lds_barrier();
+                // chunk ch+D into the slot chunk ch-1 left (every wave is past its multiply)
+                if (ch + D < nchunks) issue(ch + D);
+                if (cnt > 0)
+                    sl_segment(acc, ring_addr + (uint32_t)((ch % S) * SLOT) + (uint32_t)lane * 16,
+                               a.jt_tgt + (pass * nchunks + ch) * NW + group);
+            }
+            uint32_t rows[OPW][8];
+#pragma unroll
+            for (int o = 0; o < OPW; o++)
+#pragma unroll
+                for (int p = 0; p < 8; p++) rows[o][p] = acc[o][p];
+            const int nst = a.zero_check ? a.nstore : rbase + cnt;
+            if (a.zero_check) {
+                uint32_t any = 0;
+#pragma unroll
+                for (int o = 0; o < OPW; o++)
+                    if (o < cnt && rbase + o >= nst)
+#pragma unroll
+                        for (int p = 0; p < 8; p++) any |= rows[o][p];
+                any &= (c.vA ? 0x0F0F0F0Fu : 0u) | (c.vB ? 0xF0F0F0F0u : 0u);
+                if (__ballot(any != 0) != 0 && lane == 0) atomicAdd(a.zero_check, 1u);
+            }
+            if (rbase < nst) store_rows<OPW, true>(a, seg, c, rbase, nst - rbase < cnt ? nst - rbase : cnt, rows);
+            // the slot the next pass's first DMAs go to may still be read by a wave's multiply
+            lds_barrier();
+        }
+    }
+}
+
+template <int NW, int D>
+size_t dma_lds_bytes() {
+    return (size_t)(D + 1) * 2 * NW * 2048;
+}
+
 // Rebuild with nothing to compute (every data share present): a copy of the
 // data shares into the stripe-major segment, with no bit planes or barriers.
 // Each of the 2 waves loads all of its (up to 16) inputs of the tile before
@@ -302,6 +439,35 @@ hipError_t launch_jt_targets(const RsArgs &a, uint64_t *targets, hipStream_t s) 
     return hipGetLastError();
 }
 
+namespace {
+// chunks of LDS-DMA prefetch of the straight-line rebuild (rs_matmul_dma); 0 =
+// rs_matmul_jt's register-staged form.  Set at ec_create (UPLINK_EC_REBUILD_DEPTH)
+// for A/B builds of the library in one process.  One chunk ahead measured
+// fastest: 16 RS(29,80) segments per launch, rebuild 399.7 us at depth 1,
+// 409.4 at 2, 443.5 at 3 (each deeper slot costs the CU workgroups) and 418.5
+// register-staged (profiles/r04/exp/ab_rebuild_dma.log).
+int g_rebuild_depth = 1;
+
+template <int NW, int D>
+void launch_dma(const RsArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((rs_matmul_dma<NW, D>), dim3(grid), dim3(NW * 64), (dma_lds_bytes<NW, D>()), s, a);
+}
+
+template <int NW>
+void launch_dma_depth(const RsArgs &a, int grid, hipStream_t s, int depth) {
+    // above 4 waves the ring stays within the 64 KiB of dynamic LDS a launch gets by default
+    if constexpr (NW > 4) {
+        launch_dma<NW, 1>(a, grid, s);
+    } else {
+        if (depth <= 1) launch_dma<NW, 1>(a, grid, s);
+        else if (depth == 2) launch_dma<NW, 2>(a, grid, s);
+        else launch_dma<NW, 3>(a, grid, s);
+    }
+}
+}  // namespace
+
+void configure_rebuild(int depth) { g_rebuild_depth = depth < 0 ? 0 : depth > 3 ? 3 : depth; }
+
 template <bool SL>
 hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     if (!a.jt_tgt || a.nout > kMaxOps || a.nin > kMaxOps) return hipErrorInvalidValue;
@@ -318,6 +484,18 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     if (a.nout == 0 && !a.zero_check) {
         constexpr size_t kCopyLds = 58 * 1024;  // an occupancy cap: 2 workgroups per CU
         hipLaunchKernelGGL(rs_copy_shares<2>, dim3(grid), dim3(2 * 64), kCopyLds, s, a);
+        return hipGetLastError();
+    }
+    if (SL && g_rebuild_depth > 0) {
+        switch (sl::split_for(a.nout).nw) {
+        case 8: launch_dma_depth<8>(a, grid, s, g_rebuild_depth); break;
+        case 7: launch_dma_depth<7>(a, grid, s, g_rebuild_depth); break;
+        case 6: launch_dma_depth<6>(a, grid, s, g_rebuild_depth); break;
+        case 5: launch_dma_depth<5>(a, grid, s, g_rebuild_depth); break;
+        case 2: launch_dma_depth<2>(a, grid, s, g_rebuild_depth); break;
+        case 3: launch_dma_depth<3>(a, grid, s, g_rebuild_depth); break;
+        default: launch_dma_depth<4>(a, grid, s, g_rebuild_depth);
+        }
         return hipGetLastError();
     }
     switch (SL ? sl::split_for(a.nout).nw : jt_waves(a.nout)) {

@@ -45,6 +45,9 @@ hipError_t launch_matmul_generic(const RsArgs &args, int grid, hipStream_t strea
 // The same kernel calling a plan's straight-line segments (rs_sl.hpp):
 // args.jt_tgt = their absolute addresses, [pass][chunk][group].
 hipError_t launch_matmul_sl(const RsArgs &args, int grid, hipStream_t stream);
+// Prefetch depth of the straight-line rebuild (chunks of input shares in flight
+// by LDS-DMA; 0 = the register-staged kernel), set by ec_create.
+void configure_rebuild(int depth);
 size_t jt_targets_bytes(const RsArgs &args);
 hipError_t launch_jt_targets(const RsArgs &args, uint64_t *targets, hipStream_t stream);
 // Byte-wise fallback (any ess, any alignment); coef as above.

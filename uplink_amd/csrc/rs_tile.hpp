@@ -113,6 +113,24 @@ __device__ __forceinline__ void dma_1k(const uint8_t *g, uint32_t lds) {
         : "memory");
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63] (gfx9's 6-bit counter).
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+#define UPLINK_WAIT_VM(N) \
+    case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        UPLINK_WAIT_VM(1) UPLINK_WAIT_VM(2) UPLINK_WAIT_VM(3) UPLINK_WAIT_VM(4) UPLINK_WAIT_VM(5) UPLINK_WAIT_VM(6) UPLINK_WAIT_VM(7) UPLINK_WAIT_VM(8)
+        UPLINK_WAIT_VM(9) UPLINK_WAIT_VM(10) UPLINK_WAIT_VM(11) UPLINK_WAIT_VM(12) UPLINK_WAIT_VM(13) UPLINK_WAIT_VM(14) UPLINK_WAIT_VM(15) UPLINK_WAIT_VM(16)
+        UPLINK_WAIT_VM(17) UPLINK_WAIT_VM(18) UPLINK_WAIT_VM(19) UPLINK_WAIT_VM(20) UPLINK_WAIT_VM(21) UPLINK_WAIT_VM(22) UPLINK_WAIT_VM(23) UPLINK_WAIT_VM(24)
+        UPLINK_WAIT_VM(25) UPLINK_WAIT_VM(26) UPLINK_WAIT_VM(27) UPLINK_WAIT_VM(28) UPLINK_WAIT_VM(29) UPLINK_WAIT_VM(30) UPLINK_WAIT_VM(31) UPLINK_WAIT_VM(32)
+        UPLINK_WAIT_VM(33) UPLINK_WAIT_VM(34) UPLINK_WAIT_VM(35) UPLINK_WAIT_VM(36) UPLINK_WAIT_VM(37) UPLINK_WAIT_VM(38) UPLINK_WAIT_VM(39) UPLINK_WAIT_VM(40)
+        UPLINK_WAIT_VM(41) UPLINK_WAIT_VM(42) UPLINK_WAIT_VM(43) UPLINK_WAIT_VM(44) UPLINK_WAIT_VM(45) UPLINK_WAIT_VM(46) UPLINK_WAIT_VM(47) UPLINK_WAIT_VM(48)
+        UPLINK_WAIT_VM(49) UPLINK_WAIT_VM(50) UPLINK_WAIT_VM(51) UPLINK_WAIT_VM(52) UPLINK_WAIT_VM(53) UPLINK_WAIT_VM(54) UPLINK_WAIT_VM(55) UPLINK_WAIT_VM(56)
+        UPLINK_WAIT_VM(57) UPLINK_WAIT_VM(58) UPLINK_WAIT_VM(59) UPLINK_WAIT_VM(60) UPLINK_WAIT_VM(61) UPLINK_WAIT_VM(62) UPLINK_WAIT_VM(63)
+#undef UPLINK_WAIT_VM
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 // Checked build (UPLINK_EC_CHECKED, tests/test_c_abi.py): every 16-byte
 // global access of the stripe kernels is compared with the launch's declared
 // byte ranges; one outside them is skipped and its site recorded in
