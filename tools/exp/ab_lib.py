@@ -8,6 +8,7 @@ timed the same way; median and min over rounds.  Every build's pieces and
 rebuilds are checked against the first build's.
 
   python tools/exp/ab_lib.py LIB_A LIB_B[@VAR=VALUE,...] ... [--rounds 6] [--pairs 8]
+(VAR BODY=n is not an engine knob: ec_set_body(ctx, n) after ec_create.)
 """
 from __future__ import annotations
 
@@ -69,6 +70,8 @@ def main():
         L = load(p)
         ctx = ctypes.c_void_p()
         assert L.ec_create(K, N, ESS, ctypes.byref(ctx)) == 0
+        if "BODY" in saved:  # BODY=n: ec_set_body(ctx, n) (2 = straight-line: the SL encode for any (k, n))
+            assert L.ec_set_body(ctx, int(os.environ["BODY"])) == 0
         for var, val in saved.items():
             if val is None:
                 os.environ.pop(var)

@@ -383,7 +383,10 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // every other cycle); the 4-plane combinations each compute wave rebuilds per
 // input cost 14 % more VALU than with 4.
 constexpr int compute_waves(int k, int n) { return n - k >= 16 ? 8 : 4; }
-constexpr int loader_waves(int k, int n) { return 4; }
+#ifndef UPLINK_ENC_PARITY_NL
+#define UPLINK_ENC_PARITY_NL 4
+#endif
+constexpr int loader_waves(int k, int n) { return UPLINK_ENC_PARITY_NL; }  // -D override: A/B builds
 constexpr int parity_compute_waves(int k, int n) { return compute_waves(k, n); }
 // The full encode with at most 40 parity rows keeps 4 compute waves: its
 // loaders' copy-through share of a tile is large enough that the 4 extra

@@ -71,7 +71,7 @@ constexpr int kJtRows = 8;  // accumulator rows per wave
 // [pass][chunk][group].
 template <int NW, bool SL>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
-    constexpr int JC = 2 * NW, OPW = kJtRows, PER = 2;
+    constexpr int JC = SL ? sl::chunk_inputs(NW) : 2 * NW, OPW = kJtRows, PER = (JC + NW - 1) / NW;
     // the inputs in as few chunks of at most JC as they need, dealt evenly
     // (29 inputs on 7 waves: 10 + 10 + 9, not 14 + 14 + 1)
     const int nchunks = (a.nin + JC - 1) / JC;
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 // the pass.
 template <int NW, int D>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
-    constexpr int JC = 2 * NW, OPW = kJtRows, S = D + 1, SLOT = JC * 2048;
+    constexpr int JC = sl::chunk_inputs(NW), PER = (JC + NW - 1) / NW, OPW = kJtRows, S = D + 1, SLOT = JC * 2048;
     static_assert(D >= 1 && D <= 3, "store ring below holds at most 2 chunks");
 #ifdef UPLINK_EC_CHECKED
     constexpr bool kCountStores = false;  // the checked build may skip a store: count none (waits longer)
@@ -172,10 +172,10 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
     const uint32_t ring_addr = (uint32_t)(uintptr_t)smem;
-    // inputs of chunk ch this wave owns (j = wave, wave + NW; CH <= 2 NW)
+    // inputs of chunk ch this wave owns (j = wave, wave + NW, ...; CH <= JC)
     auto owned = [&](int ch) -> int {
         const int jn = a.nin - ch * CH < CH ? a.nin - ch * CH : CH;
-        return (wave < jn ? 1 : 0) + (wave + NW < jn ? 1 : 0);
+        return wave < jn ? (jn - wave + NW - 1) / NW : 0;
     };
     for (int64_t tile = blockIdx.x; tile < a.total_tiles; tile += gridDim.x) {
         const int64_t seg = tile / a.tiles_per_seg;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
             const uint32_t d0 = ring_addr + (uint32_t)((ch % S) * SLOT);
             const int j0 = ch * CH;
 #pragma unroll
-            for (int i = 0; i < 2; i++) {
+            for (int i = 0; i < PER; i++) {
                 const int j = wave + NW * i;
                 if (i < owned(ch)) {
                     const uint8_t *p = in_seg + a.in_off[j0 + j];
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
                 u32x4 *slot = ring + (ch % S) * (SLOT / 16);
                 int st = 0;
 #pragma unroll
-                for (int i = 0; i < 2; i++) {
+                for (int i = 0; i < PER; i++) {
                     const int j = wave + NW * i;
                     if (i < owned(ch)) {
                         const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
 
 template <int NW, int D>
 size_t dma_lds_bytes() {
-    return (size_t)(D + 1) * 2 * NW * 2048;
+    return (size_t)(D + 1) * sl::chunk_inputs(NW) * 2048;
 }
 
 // Rebuild with nothing to compute (every data share present): a copy of the
@@ -324,9 +324,9 @@ __global__ __launch_bounds__(NW * 64) void rs_copy_shares(const RsArgs a) {
     }
 }
 
-template <int NW>
+template <int NW, bool SL = true>
 size_t jt_lds_bytes(const RsArgs &) {
-    return (size_t)2 * 2 * NW * 8 * 64 * 4;
+    return (size_t)2 * (SL ? sl::chunk_inputs(NW) : 2 * NW) * 8 * 64 * 4;
 }
 
 int jt_waves(int nout) { return nout <= 2 * kJtRows ? 2 : nout <= 3 * kJtRows ? 3 : 4; }
@@ -512,13 +512,13 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
         hipLaunchKernelGGL((rs_matmul_jt<5, true>), dim3(grid), dim3(5 * 64), jt_lds_bytes<5>(a), s, a);
         break;
     case 2:
-        hipLaunchKernelGGL((rs_matmul_jt<2, SL>), dim3(grid), dim3(2 * 64), jt_lds_bytes<2>(a), s, a);
+        hipLaunchKernelGGL((rs_matmul_jt<2, SL>), dim3(grid), dim3(2 * 64), (jt_lds_bytes<2, SL>(a)), s, a);
         break;
     case 3:
-        hipLaunchKernelGGL((rs_matmul_jt<3, SL>), dim3(grid), dim3(3 * 64), jt_lds_bytes<3>(a), s, a);
+        hipLaunchKernelGGL((rs_matmul_jt<3, SL>), dim3(grid), dim3(3 * 64), (jt_lds_bytes<3, SL>(a)), s, a);
         break;
     default:
-        hipLaunchKernelGGL((rs_matmul_jt<4, SL>), dim3(grid), dim3(4 * 64), jt_lds_bytes<4>(a), s, a);
+        hipLaunchKernelGGL((rs_matmul_jt<4, SL>), dim3(grid), dim3(4 * 64), (jt_lds_bytes<4, SL>(a)), s, a);
     }
     return hipGetLastError();
 }

@@ -23,8 +23,8 @@
 // byte address of the chunk's first input for this lane, in the wide layout of
 // rs_device.hpp slice_inputs (input jj at +2048 jj, planes 0-3 of the lane as
 // one 16-byte word at +0, planes 4-7 at +1024; the lane's 16 bytes are folded
-// into v126); return address s[48:49].  A chunk is at most 2 * nw inputs; the
-// inputs are dealt evenly over ceil(nin / (2 nw)) chunks.
+// into v126); return address s[48:49].  A chunk is at most chunk_inputs(nw)
+// inputs; the inputs are dealt evenly over ceil(nin / chunk_inputs(nw)) chunks.
 // Generated code touches nothing else: no memory but LDS reads, no scalar
 // registers, no M0.
 #pragma once
@@ -58,6 +58,16 @@ struct Split {
     int count(int pass, int g, int rows) const;
 };
 Split split_for(int rows);  // the kernel launch (launch_matmul_sl) uses the same split
+
+// Inputs per chunk (the most; the inputs are dealt evenly over
+// ceil(nin / chunk_inputs) chunks): 2 per wave.  -DUPLINK_SL_CHUNK2 sets the
+// 2-wave figure for A/B builds: 4, 6 or 8 inputs (RS(29,80) in 8, 5 or 4
+// chunks, each a barrier and a round trip to memory) rebuild within 0.2 %
+// of each other (profiles/r04/exp/ab_chunk.log).
+#ifndef UPLINK_SL_CHUNK2
+#define UPLINK_SL_CHUNK2 4
+#endif
+constexpr int chunk_inputs(int nw) { return nw == 2 ? UPLINK_SL_CHUNK2 : 2 * nw; }
 
 // Generate the segments of M (rows x nin, row-major) into `code` (cap words,
 // pre-filled by the caller).  seg_off receives, for [pass][chunk][group], the

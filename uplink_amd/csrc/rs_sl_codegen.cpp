@@ -145,7 +145,7 @@ Split split_for(int rows) {
 
 size_t generate(const uint8_t *M, int rows, int nin, uint32_t *code, size_t cap, std::vector<uint32_t> &seg_off) {
     const Split sp = split_for(rows);
-    const int jc = 2 * sp.nw, nchunks = (nin + jc - 1) / jc, ch_size = (nin + nchunks - 1) / nchunks;
+    const int jc = chunk_inputs(sp.nw), nchunks = (nin + jc - 1) / jc, ch_size = (nin + nchunks - 1) / nchunks;
     seg_off.assign((size_t)sp.npass * nchunks * sp.nw, kNoSegment);
     Emitter e{code, cap};
     // the region's first 64 words stay s_endpgm: no segment starts at offset 0
