@@ -53,7 +53,7 @@ res = {
               "over dispatches; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py",
     "segments_per_launch": B,
     "encode": family("rs_encode_special<29, 80, 8, 4, true>"),
-    "decode": family("rs_matmul_jt"),
+    "decode": family("rs_matmul_dma"),  # the straight-line rebuild (a plan's first launch: rs_matmul_jt)
     "encode_parity_only": family("rs_encode_special<29, 80, 8, 4, false>"),
     "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD,
                     "encode_parity_only": int(B * S_PAD * (1 + (N - K) / K))},
