@@ -100,6 +100,7 @@ def main():
         print(f"{tag:24s} build {bid} results {'match' if ok else 'DIFFER'}", flush=True)
         builds.append((tag, L, ctx))
     counter = [0]
+    per_set = {}  # library -> share set -> rebuild us per launch
 
     def run(L, ctx, flags):
         evs = []
@@ -114,10 +115,13 @@ def main():
             assert L.ec_rebuild_segments_batched(ctx, K, nums_c[i], ptrs_c[i], NSTRIPES, B, N * PIECE, S_PAD,
                                                  outs.data_ptr(), sptr) == 0
             e[2].record(stream)
-            evs.append(e)
+            evs.append((e, i))
         torch.cuda.synchronize()
-        enc = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) * 1e3
-        dec = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs) * 1e3
+        enc = sum(e[0].elapsed_time(e[1]) for e, _ in evs) / len(evs) * 1e3
+        dec = sum(e[1].elapsed_time(e[2]) for e, _ in evs) / len(evs) * 1e3
+        if not flags:
+            for e, i in evs:
+                per_set.setdefault(L, {}).setdefault(i, []).append(e[1].elapsed_time(e[2]) * 1e3)
         return enc, dec
 
     t0 = time.perf_counter()  # settle the clocks
@@ -142,6 +146,13 @@ def main():
         print(f"{tag:24s} encode {e:7.1f} ({min(v['enc']):7.1f}) {eb / e / 8e6:.4f}   rebuild {d:6.1f} "
               f"({min(v['dec']):6.1f}) {db / d / 8e6:.4f}   parity-only {p:6.1f} ({min(v['par']):6.1f}) "
               f"{pb / p / 8e6:.4f}", flush=True)
+    print("rebuild us per launch by share set (m = missing data shares), median over the run")
+    for tag, L, _ in builds:
+        row = []
+        for i, v in sorted(per_set.get(L, {}).items()):
+            m = K - sum(1 for x in sets[i] if x < K)
+            row.append(f"m={m}:{sorted(v)[len(v) // 2]:.1f}")
+        print(f"{tag:24s} " + " ".join(row), flush=True)
 
 
 if __name__ == "__main__":

@@ -136,9 +136,14 @@ int Split::count(int pass, int g, int rows) const {
 
 Split split_for(int rows) {
     Split s;
-    // 2-4 waves as the jump table; past 32 rows up to 8 waves (2 workgroups
-    // per CU), so up to 64 rows take one pass over the inputs
-    s.nw = rows <= 2 * kRows ? 2 : rows <= 3 * kRows ? 3 : rows >= 8 * kRows ? 8 : (rows + kRows - 1) / kRows;
+    // 2-4 waves; past 32 rows up to 8 waves (2 workgroups per CU), so up to 64
+    // rows take one pass over the inputs.  15-16 rows on 3 waves (5-6 rows each), not 2 (8 each): RS(29,80) m = 16 394 vs
+    // 401-405 us per 16 segments (profiles/r04/exp/ab_rows_per_wave.log); 25-32 rows stay on
+    // 4 waves (5 waves: 590-614 against 412 us at m = 29, register-staged or not)
+#ifndef UPLINK_SL_TWO_WAVE_ROWS
+#define UPLINK_SL_TWO_WAVE_ROWS 14
+#endif
+    s.nw = rows <= UPLINK_SL_TWO_WAVE_ROWS ? 2 : rows <= 3 * kRows ? 3 : rows >= 8 * kRows ? 8 : (rows + kRows - 1) / kRows;
     s.npass = rows > 0 ? (rows + s.nw * kRows - 1) / (s.nw * kRows) : 1;
     return s;
 }
