@@ -44,6 +44,16 @@ using namespace dev;
 #ifndef UPLINK_ENC_MAX_CHUNK
 #define UPLINK_ENC_MAX_CHUNK 36
 #endif
+// compute waves (from 16 parity rows on), loader waves and workgroups per CU
+#ifndef UPLINK_ENC_NC
+#define UPLINK_ENC_NC 8
+#endif
+#ifndef UPLINK_ENC_PARITY_NL
+#define UPLINK_ENC_PARITY_NL 4
+#endif
+#ifndef UPLINK_ENC_WGS
+#define UPLINK_ENC_WGS 1
+#endif
 constexpr int kSlots = UPLINK_ENC_SLOTS;
 constexpr int kAhead = kSlots - 1;               // items between a load's issue and that item's multiply
 constexpr int kMaxChunk = UPLINK_ENC_MAX_CHUNK;  // input shares per item
@@ -371,7 +381,8 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
 }
 
 template <int K, int N, int NC, int NL, bool COPY>
-__global__ __launch_bounds__((NC + NL) * 64, 1) void rs_encode_special(const RsArgs a) {
+__global__ __launch_bounds__((NC + NL) * 64, UPLINK_ENC_WGS > 1 ? (NC + NL) * UPLINK_ENC_WGS / 4 : 1) void rs_encode_special(
+    const RsArgs a) {
     encode_body<K, N, NC, NL, COPY, 0>(a);
 }
 
@@ -382,10 +393,7 @@ constexpr bool supported(int k, int n) { return k >= 1 && k <= kMaxOps && n - k 
 // SIMD, so each issues VALU at the full rate (one wave alone on a SIMD issues
 // every other cycle); the 4-plane combinations each compute wave rebuilds per
 // input cost 14 % more VALU than with 4.
-constexpr int compute_waves(int k, int n) { return n - k >= 16 ? 8 : 4; }
-#ifndef UPLINK_ENC_PARITY_NL
-#define UPLINK_ENC_PARITY_NL 4
-#endif
+constexpr int compute_waves(int k, int n) { return n - k >= 16 ? UPLINK_ENC_NC : 4; }  // -D override: A/B builds
 constexpr int loader_waves(int k, int n) { return UPLINK_ENC_PARITY_NL; }  // -D override: A/B builds
 constexpr int parity_compute_waves(int k, int n) { return compute_waves(k, n); }
 // The full encode with at most 40 parity rows keeps 4 compute waves: its
@@ -395,7 +403,7 @@ constexpr int parity_compute_waves(int k, int n) { return compute_waves(k, n); }
 constexpr int full_compute_waves(int k, int n) { return n - k <= 40 ? 4 : compute_waves(k, n); }
 constexpr int full_loader_waves(int k, int n) { return loader_waves(k, n); }
 // One workgroup per CU: its ring takes up to 144 KiB of LDS.
-constexpr int wgs_per_cu(int k, int waves) { return 1; }
+constexpr int wgs_per_cu(int k, int waves) { return UPLINK_ENC_WGS; }
 
 }  // namespace enc
 }  // namespace uplink_ec
