@@ -143,7 +143,11 @@ Split split_for(int rows) {
 #ifndef UPLINK_SL_TWO_WAVE_ROWS
 #define UPLINK_SL_TWO_WAVE_ROWS 14
 #endif
-    s.nw = rows <= UPLINK_SL_TWO_WAVE_ROWS ? 2 : rows <= 3 * kRows ? 3 : rows >= 8 * kRows ? 8 : (rows + kRows - 1) / kRows;
+#ifndef UPLINK_SL_WIDE_ROWS_PER_WAVE  // rows per wave past 24 rows (A/B builds; at most kRows)
+#define UPLINK_SL_WIDE_ROWS_PER_WAVE 8
+#endif
+    constexpr int RW = UPLINK_SL_WIDE_ROWS_PER_WAVE;
+    s.nw = rows <= UPLINK_SL_TWO_WAVE_ROWS ? 2 : rows <= 3 * kRows ? 3 : rows >= 8 * RW ? 8 : (rows + RW - 1) / RW;
     s.npass = rows > 0 ? (rows + s.nw * kRows - 1) / (s.nw * kRows) : 1;
     return s;
 }
