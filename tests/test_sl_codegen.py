@@ -238,10 +238,10 @@ def test_region_sizes():
 def test_wave_split_by_row_count():
     """The row split the kernel launch and the code generator share (split_for,
     rs_sl_codegen.cpp): 2 waves up to 14 rows, 3 up to 24 (RS(29,80) m = 16
-    on 3, DESIGN.md §4 "Rebuild, round 4"), 4 up to 32, then 8 rows per wave,
-    8 waves and several passes past 64 rows; chunks of 2 inputs per wave."""
+    on 3, DESIGN.md §4 "Rebuild, round 4"), 4 up to 32, 8 past that (one pass
+    up to 64 rows, several beyond); chunks of 2 inputs per wave."""
     want = {1: (2, 1), 14: (2, 1), 15: (3, 1), 16: (3, 1), 24: (3, 1), 25: (4, 1), 29: (4, 1), 32: (4, 1),
-            33: (5, 1), 64: (8, 1), 65: (8, 2), 128: (8, 2)}
+            33: (8, 1), 40: (8, 1), 64: (8, 1), 65: (8, 2), 128: (8, 2)}
     for rows, (nw, npass) in want.items():
         got = generate(np.ones((rows, 29), dtype=np.uint8))
         assert got[:2] == (nw, npass), rows

@@ -136,18 +136,26 @@ int Split::count(int pass, int g, int rows) const {
 
 Split split_for(int rows) {
     Split s;
-    // 2-4 waves; past 32 rows up to 8 waves (2 workgroups per CU), so up to 64
-    // rows take one pass over the inputs.  15-16 rows on 3 waves (5-6 rows each), not 2 (8 each): RS(29,80) m = 16 394 vs
-    // 401-405 us per 16 segments (profiles/r04/exp/ab_rows_per_wave.log); 25-32 rows stay on
-    // 4 waves (5 waves: 590-614 against 412 us at m = 29, register-staged or not)
+    // 2-4 waves up to 32 rows, 8 past them (2 workgroups per CU), so up to 64
+    // rows take one pass over the inputs.  15-16 rows on 3 waves (5-6 rows
+    // each), not 2 (8 each): RS(29,80) m = 16 394 vs 401-405 us per 16 segments
+    // (profiles/r04/exp/ab_rows_per_wave.log).  Not 5-7 waves: a 127-VGPR wave
+    // leaves a CU 16 wave slots, which 5-wave workgroups fill to about 10 (SQ
+    // wave cycles), so m = 29 on 5 waves took 590-614 against 412 us on 4, and
+    // Decode at k+20 (33-40 rows) 48 against 43 us per segment on 8
+    // (profiles/r04/exp/nw8_decode.log).  -D overrides for A/B builds.
 #ifndef UPLINK_SL_TWO_WAVE_ROWS
 #define UPLINK_SL_TWO_WAVE_ROWS 14
 #endif
-#ifndef UPLINK_SL_WIDE_ROWS_PER_WAVE  // rows per wave past 24 rows (A/B builds; at most kRows)
-#define UPLINK_SL_WIDE_ROWS_PER_WAVE 8
+#ifndef UPLINK_SL_WIDE_ROWS_PER_WAVE  // rows per wave past 32 rows (at most kRows)
+#define UPLINK_SL_WIDE_ROWS_PER_WAVE 4
 #endif
     constexpr int RW = UPLINK_SL_WIDE_ROWS_PER_WAVE;
-    s.nw = rows <= UPLINK_SL_TWO_WAVE_ROWS ? 2 : rows <= 3 * kRows ? 3 : rows >= 8 * RW ? 8 : (rows + RW - 1) / RW;
+    s.nw = rows <= UPLINK_SL_TWO_WAVE_ROWS ? 2
+           : rows <= 3 * kRows                ? 3
+           : rows <= 4 * kRows                ? 4
+           : rows >= 8 * RW                   ? 8
+                                              : (rows + RW - 1) / RW;
     s.npass = rows > 0 ? (rows + s.nw * kRows - 1) / (s.nw * kRows) : 1;
     return s;
 }
