@@ -124,7 +124,8 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     constexpr int S = enc::kDiagStamp, NP = enc::kDiagNoParityStores, NCP = enc::kDiagNoCopyStores;
-    constexpr int NCB = enc::kDiagNoCombos, NR = enc::kDiagNoRowOps, HC = enc::kDiagHalfCombos;
+    constexpr int NCB = enc::kDiagNoCombos, NR = enc::kDiagNoRowOps, HC = enc::kDiagHalfCombos,
+                  LC = enc::kDiagLdsCombos;
     const Variant vars[] = {
         {"full", true, 0, launch<true, 0>},
         {"full stamp", true, S, launch<true, S>},
@@ -135,6 +136,7 @@ int main(int argc, char **argv) {
         {"full norowops", true, S | NR, launch<true, S | NR>},
         {"full norow+nost", true, S | NR | NP | NCP, launch<true, S | NR | NP | NCP>},
         {"full halfcombo", true, S | HC, launch<true, S | HC>},
+        {"full ldscombo", true, S | LC, launch<true, S | LC>},
         {"full 4c+4l", true, S, launch<true, S, 4, 4>},
         {"full 6c+4l", true, S, launch<true, S, 6, 4>},
         {"full 6c+6l", true, S, launch<true, S, 6, 6>},
@@ -145,6 +147,7 @@ int main(int argc, char **argv) {
         {"parity nocombo", false, S | NCB, launch<false, S | NCB>},
         {"parity norowops", false, S | NR, launch<false, S | NR>},
         {"parity halfcombo", false, S | HC, launch<false, S | HC>},
+        {"parity ldscombo", false, S | LC, launch<false, S | LC>},
         {"parity 4c+4l", false, S, launch<false, S, 4, 4>},
         {"parity 6c+4l", false, S, launch<false, S, 6, 4>},
     };

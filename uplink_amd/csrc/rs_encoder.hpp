@@ -78,12 +78,26 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
     asm volatile("" : "+s"(opq));
     slot += opq;
     u32x4 nlo = slot[lane], nhi = slot[64 + lane];
+    // kDiagLdsCombos: the 30 combination planes of the next input, read ahead from the LDS
+    constexpr bool kLdsCombos = (DIAG & 64) != 0;
+    constexpr int kCbSpan = JN * 128 > 1024 ? JN * 128 - 512 : 1;
+    [[maybe_unused]] u32x4 ncb[8];
+    if constexpr (kLdsCombos)
+#pragma unroll
+        for (int q = 0; q < 8; q++) ncb[q] = slot[(q * 64) % (JN * 128) + lane];
     static_for<JN>([&]<int JJ>() {
         constexpr int J = J0 + JJ;
         const u32x4 lo4 = nlo, hi4 = nhi;
+        [[maybe_unused]] u32x4 cb[8];
+        if constexpr (kLdsCombos)
+#pragma unroll
+            for (int q = 0; q < 8; q++) cb[q] = ncb[q];
         if constexpr (JJ + 1 < JN) {
             nlo = slot[(JJ + 1) * 128 + lane];
             nhi = slot[(JJ + 1) * 128 + 64 + lane];
+            if constexpr (kLdsCombos)
+#pragma unroll
+                for (int q = 0; q < 8; q++) ncb[q] = slot[((JJ + 1) * 512 % kCbSpan + q * 64) % (JN * 128) + lane];
         }
         asm volatile("" ::: "memory");
         const uint32_t x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
@@ -94,6 +108,13 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
         uint32_t lo[16], hi[16];
         lo[0] = 0;
         hi[0] = 0;
+        if constexpr (kLdsCombos) {  // timing only: every entry from the LDS reads (values meaningless)
+            static_for<15>([&]<int M1>() {
+                constexpr int a = M1, b = M1 + 15;
+                lo[M1 + 1] = cb[a / 4][a % 4];
+                hi[M1 + 1] = cb[b / 4][b % 4];
+            });
+        } else
         static_for<15>([&]<int M1>() {
             constexpr int M = M1 + 1;
             constexpr int low = M & (-M);
@@ -151,8 +172,11 @@ __device__ __forceinline__ int32_t take_tile(const RsArgs &a, int m) {
 //                         are read from the LDS and kept live, the rows stay zero)
 //   kDiagHalfCombos       timing only: kDiagNoCombos for the odd inputs (what
 //                         building each input's combinations in half the waves saves)
+//   kDiagLdsCombos        timing only: the 30 combination planes of each input read
+//                         from the LDS (8 ds_read_b128 per lane, one input ahead)
+//                         instead of built (what publishing them once per tile would cost)
 constexpr int kDiagStamp = 1, kDiagNoParityStores = 2, kDiagNoCopyStores = 4, kDiagNoCombos = 8, kDiagNoRowOps = 16,
-              kDiagHalfCombos = 32;
+              kDiagHalfCombos = 32, kDiagLdsCombos = 64;
 
 __device__ __forceinline__ void sink16(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     asm volatile("" ::"v"(x), "v"(y), "v"(z), "v"(w));
