@@ -154,9 +154,12 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 // rewrites column 0 with the bytes already there), so each wave's count of
 // VMEM operations is exact.  Each pass's pipeline starts and drains within
 // the pass.
-template <int NW, int D>
+// SL = false: the same pipeline around the jump-table body (a plan's first
+// launch), its planes sliced into the narrow layout (plane p at 256 p + 4 lane).
+template <int NW, int D, bool SL = true>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
-    constexpr int JC = sl::chunk_inputs(NW), PER = (JC + NW - 1) / NW, OPW = kJtRows, S = D + 1, SLOT = JC * 2048;
+    constexpr int JC = SL ? sl::chunk_inputs(NW) : 2 * NW, PER = (JC + NW - 1) / NW, OPW = kJtRows, S = D + 1,
+                  SLOT = JC * 2048;
     static_assert(D >= 1 && D <= 3, "store ring below holds at most 2 chunks");
 #ifdef UPLINK_EC_CHECKED
     constexpr bool kCountStores = false;  // the checked build may skip a store: count none (waits longer)
@@ -239,8 +242,16 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
                         }
                         uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
                         bitslice8(w);
-                        slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
-                        slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
+                        if constexpr (SL) {
+                            slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
+                            slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
+                        } else {
+                            // the wave read all of its input's raw bytes above (LDS operations of a
+                            // wave complete in order), so the narrow layout may overwrite them
+                            uint32_t *np = (uint32_t *)(slot + j * 128) + lane;
+#pragma unroll
+                            for (int q = 0; q < 8; q++) np[q * 64] = w[q];
+                        }
                     }
                 }
                 st2 = st1;
@@ -248,9 +259,17 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
                 lds_barrier();
                 // chunk ch+D into the slot chunk ch-1 left (every wave is past its multiply)
                 if (ch + D < nchunks) issue(ch + D);
-                if (cnt > 0)
-                    sl_segment(acc, ring_addr + (uint32_t)((ch % S) * SLOT) + (uint32_t)lane * 16,
-                               a.jt_tgt + (pass * nchunks + ch) * NW + group);
+                if (cnt > 0) {
+                    if constexpr (SL) {
+                        sl_segment(acc, ring_addr + (uint32_t)((ch % S) * SLOT) + (uint32_t)lane * 16,
+                                   a.jt_tgt + (pass * nchunks + ch) * NW + group);
+                    } else {
+                        const int jn = a.nin - j0 < CH ? a.nin - j0 : CH;
+                        jt_inputs(acc, ring_addr + (uint32_t)((ch % S) * SLOT) + (uint32_t)lane * 4,
+                                  a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
+                                  (uint32_t)(OPW - cnt), (uint32_t)jn);
+                    }
+                }
             }
             uint32_t rows[OPW][8];
 #pragma unroll
@@ -275,9 +294,9 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
     }
 }
 
-template <int NW, int D>
+template <int NW, int D, bool SL = true>
 size_t dma_lds_bytes() {
-    return (size_t)(D + 1) * sl::chunk_inputs(NW) * 2048;
+    return (size_t)(D + 1) * (SL ? sl::chunk_inputs(NW) : 2 * NW) * 2048;
 }
 
 // Rebuild with nothing to compute (every data share present): a copy of the
@@ -448,9 +467,9 @@ namespace {
 // register-staged (profiles/r04/exp/ab_rebuild_dma.log).
 int g_rebuild_depth = 1;
 
-template <int NW, int D>
+template <int NW, int D, bool SL = true>
 void launch_dma(const RsArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((rs_matmul_dma<NW, D>), dim3(grid), dim3(NW * 64), (dma_lds_bytes<NW, D>()), s, a);
+    hipLaunchKernelGGL((rs_matmul_dma<NW, D, SL>), dim3(grid), dim3(NW * 64), (dma_lds_bytes<NW, D, SL>()), s, a);
 }
 
 template <int NW>
@@ -484,6 +503,14 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     if (a.nout == 0 && !a.zero_check) {
         constexpr size_t kCopyLds = 58 * 1024;  // an occupancy cap: 2 workgroups per CU
         hipLaunchKernelGGL(rs_copy_shares<2>, dim3(grid), dim3(2 * 64), kCopyLds, s, a);
+        return hipGetLastError();
+    }
+    if (!SL && g_rebuild_depth > 0) {  // the jump-table body (2-4 waves), one chunk ahead
+        switch (jt_waves(a.nout)) {
+        case 2: launch_dma<2, 1, false>(a, grid, s); break;
+        case 3: launch_dma<3, 1, false>(a, grid, s); break;
+        default: launch_dma<4, 1, false>(a, grid, s);
+        }
         return hipGetLastError();
     }
     if (SL && g_rebuild_depth > 0) {
