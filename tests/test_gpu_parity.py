@@ -541,19 +541,21 @@ def test_rebuild_every_missing_count(oracle, k, n, body):
 
 @pytest.mark.parametrize("depth", [0, 2, 3])
 def test_rebuild_prefetch_depths_bit_exact(oracle, monkeypatch, depth):
-    """The straight-line rebuild's input pipeline (rs_matmul_dma: LDS-DMA of
-    the next chunk(s) of input shares, counted vmcnt waits, in-place slicing)
-    at every prefetch depth the library builds, and the register-staged kernel
-    (depth 0), against the segment: every missing count of RS(29,80) and
+    """The rebuild's input pipeline (rs_matmul_dma: LDS-DMA of the next
+    chunk(s) of input shares, counted vmcnt waits, in-place slicing) at every
+    prefetch depth the library builds, and the register-staged kernel (depth
+    0), straight-line and jump-table bodies, against the segment: every missing count of RS(29,80) and
     RS(50,80) (2-4 waves), a 2-segment batch with a ragged last tile, and an
     RS(128,256) parity-heavy set (8 waves, two passes).  The depth is set at
     ec_create and is library-wide, so the test ends by creating a context at
     the default depth again."""
     monkeypatch.setenv("UPLINK_EC_REBUILD_DEPTH", str(depth))
     try:
-        for k, n, stripes, nseg in [(29, 80, 41, 2), (50, 80, 9, 1)]:
+        for k, n, stripes, nseg, body in [(29, 80, 41, 2, _native.EC_BODY_STRAIGHT_LINE),
+                                          (29, 80, 41, 2, _native.EC_BODY_JUMP_TABLE),
+                                          (50, 80, 9, 1, _native.EC_BODY_STRAIGHT_LINE)]:
             sch = scheme(k, n, 256)
-            assert sch._lib.ec_set_body(sch._ctx, _native.EC_BODY_STRAIGHT_LINE) == 0
+            assert sch._lib.ec_set_body(sch._ctx, body) == 0
             rng = np.random.default_rng(depth * 100 + k)
             seg = rng.integers(0, 256, nseg * stripes * k * 256, dtype=np.uint8)
             d_pieces = gpu_encode(sch, seg, nseg=nseg)
