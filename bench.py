@@ -7,16 +7,16 @@ segments, sharded contiguously over the ranks (uplink_amd/shard.py:
 128 per GPU at 8 GPUs) with no collective on the data path.
 
 One step = every rank processes its whole shard once, in launches of
-`--batch` (default 16) segments, each launch pair being
-  1. ec_encode_segments: 16 segments -> 80 pieces of 2,314,240 B each
+`--batch` (default 32) segments, each launch pair being
+  1. ec_encode_segments: 32 segments -> 80 pieces of 2,314,240 B each
      (segmentupload/encode.go:39-75 for all pieces at once);
-  2. ec_rebuild_segments_batched: the 16 segments rebuilt from exactly 29 of
+  2. ec_rebuild_segments_batched: the 32 segments rebuilt from exactly 29 of
      their pieces (stripe.go:382-428 for all stripes at once).  The 29-piece
      set cycles per launch through {51..79} (all parity, worst case) and seven
      seeded random 29-subsets (default_rng(29)); decode plans are made in the
      untimed warm-up.
 The segments are synthetic (device-generated random bytes, PadReader-padded to
-9040 stripes x 29 x 256 B), from a pool of 2 x 16 distinct segments per rank
+9040 stripes x 29 x 256 B), from a pool of 2 x 32 distinct segments per rank
 cycled over the shard: 1024 segments' pieces would not fit one GPU (SURVEY §8d
 C4).  value = (payload bytes S_pad of all segments of all ranks, all steps) /
 (max over ranks of the timed wall time) in GiB/s, i.e. S_pad / (t_encode +
@@ -67,8 +67,8 @@ def parse():
                          "ramp for tens of ms under sustained load (DESIGN.md §5)")
     ap.add_argument("--total-segments", type=int, default=1024,
                     help="BASELINE configs[3]: segments per step over all ranks (sharded contiguously)")
-    ap.add_argument("--batch", type=int, default=16,
-                    help="segments per launch (12-16 measured best on MI355X, DESIGN.md §5)")
+    ap.add_argument("--batch", type=int, default=32,
+                    help="segments per launch (32: +1.3 %% over 16, the rebuild's grid twice as long; DESIGN.md §5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the RS(20,50)/(30,60)/(50,80) entries (PMC passes: only RS(29,80) launches)")
@@ -647,7 +647,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (device-generated random segments, PadReader-padded; pool of 2 x 16 per rank, cycled)",
+        "data": f"synthetic (device-generated random segments, PadReader-padded; pool of 2 x {B} per rank, cycled)",
         "config": {"workload": "RS(29,80) encode+decode of a batch of 64 MiB segments sharded over the GPUs "
                                "(BASELINE configs[3], each segment as configs[1]+[2])",
                    "k": K, "n": N, "erasure_share_size": ESS, "total_segments_per_step": args.total_segments,

@@ -121,7 +121,8 @@ def test_bench_configs3_eight_ranks_on_one_gpu():
     env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "8", "--steps",
-           "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline", "--no-other-configs"]
+           "1", "--warmup", "1", "--settle-s", "0", "--no-cpu-baseline", "--no-other-configs",
+           "--batch", "16"]  # eight ranks' pools on one GPU: 2 x 16 segments each
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])

@@ -10,7 +10,7 @@ import sys
 from collections import defaultdict
 
 fetch_dir, write_dir, out = sys.argv[1:4]
-B = int(sys.argv[4]) if len(sys.argv) > 4 else 16  # segments per launch (bench.py --batch)
+B = int(sys.argv[4]) if len(sys.argv) > 4 else 32  # segments per launch (bench.py --batch default)
 K, N, S_PAD = 29, 80, 9040 * 29 * 256
 
 
