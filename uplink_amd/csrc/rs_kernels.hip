@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "gf256_field.hpp"
 #include "rs_device.hpp"
@@ -465,7 +466,7 @@ namespace {
 // fastest: 16 RS(29,80) segments per launch, rebuild 399.7 us at depth 1,
 // 409.4 at 2, 443.5 at 3 (each deeper slot costs the CU workgroups) and 418.5
 // register-staged (profiles/r04/exp/ab_rebuild_dma.log).
-int g_rebuild_depth = 1;
+std::atomic<int> g_rebuild_depth{1};  // written by ec_create, read by launches on any thread
 
 template <int NW, int D, bool SL = true>
 void launch_dma(const RsArgs &a, int grid, hipStream_t s) {
@@ -485,7 +486,7 @@ void launch_dma_depth(const RsArgs &a, int grid, hipStream_t s, int depth) {
 }
 }  // namespace
 
-void configure_rebuild(int depth) { g_rebuild_depth = depth < 0 ? 0 : depth > 3 ? 3 : depth; }
+void configure_rebuild(int depth) { g_rebuild_depth.store(depth < 0 ? 0 : depth > 3 ? 3 : depth); }
 
 template <bool SL>
 hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
@@ -505,7 +506,8 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
         hipLaunchKernelGGL(rs_copy_shares<2>, dim3(grid), dim3(2 * 64), kCopyLds, s, a);
         return hipGetLastError();
     }
-    if (!SL && g_rebuild_depth > 0) {  // the jump-table body (2-4 waves), one chunk ahead
+    const int depth = g_rebuild_depth.load(std::memory_order_relaxed);
+    if (!SL && depth > 0) {  // the jump-table body (2-4 waves), one chunk ahead
         switch (jt_waves(a.nout)) {
         case 2: launch_dma<2, 1, false>(a, grid, s); break;
         case 3: launch_dma<3, 1, false>(a, grid, s); break;
@@ -513,15 +515,15 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    if (SL && g_rebuild_depth > 0) {
+    if (SL && depth > 0) {
         switch (sl::split_for(a.nout).nw) {
-        case 8: launch_dma_depth<8>(a, grid, s, g_rebuild_depth); break;
-        case 7: launch_dma_depth<7>(a, grid, s, g_rebuild_depth); break;
-        case 6: launch_dma_depth<6>(a, grid, s, g_rebuild_depth); break;
-        case 5: launch_dma_depth<5>(a, grid, s, g_rebuild_depth); break;
-        case 2: launch_dma_depth<2>(a, grid, s, g_rebuild_depth); break;
-        case 3: launch_dma_depth<3>(a, grid, s, g_rebuild_depth); break;
-        default: launch_dma_depth<4>(a, grid, s, g_rebuild_depth);
+        case 8: launch_dma_depth<8>(a, grid, s, depth); break;
+        case 7: launch_dma_depth<7>(a, grid, s, depth); break;
+        case 6: launch_dma_depth<6>(a, grid, s, depth); break;
+        case 5: launch_dma_depth<5>(a, grid, s, depth); break;
+        case 2: launch_dma_depth<2>(a, grid, s, depth); break;
+        case 3: launch_dma_depth<3>(a, grid, s, depth); break;
+        default: launch_dma_depth<4>(a, grid, s, depth);
         }
         return hipGetLastError();
     }
