@@ -366,10 +366,12 @@ def fresh_share_sets(L, dev, sptr, nb: int = 16, launches: int = 12):
             torch.cuda.synchronize()
         fresh = (time.perf_counter() - t0) / launches
         t0 = time.perf_counter()
-        for s in sets:  # the same sets again: the plan's generated code is made now
+        for s in sets:  # the same sets again (their generated code is being made in the background)
             run(s, n)
             torch.cuda.synchronize()
         second = (time.perf_counter() - t0) / launches
+        for s in sets:  # (wait for the background builder: the warm launches run the generated code)
+            L.ec_prepare_rebuild(ctx, K, (ctypes.c_int * K)(*s), 1)
         t0 = time.perf_counter()
         for s in sets:  # and once more: plans and code warm
             run(s, n)
@@ -378,11 +380,88 @@ def fresh_share_sets(L, dev, sptr, nb: int = 16, launches: int = 12):
         res[f"{n} segment(s) per launch"] = {"first_launch_us": round(fresh * 1e6, 1),
                                              "second_launch_us": round(second * 1e6, 1),
                                              "warm_launch_us": round(warm * 1e6, 1)}
-    res["note"] = ("EC_BODY_AUTO: a plan's first launch runs the jump table (no code generation or module "
-                   "load), its second makes and runs the plan's straight-line code")
+    res["note"] = ("ec_rebuild_segments_batched, EC_BODY_AUTO: a share set without generated code runs the "
+                   "share-set pass (decode rows solved on the GPU, jump-table body) and has its straight-line code "
+                   "made in the background; warm = after ec_prepare_rebuild(wait)")
     del segs, pcs, back
     L.ec_destroy(ctx)
     return res
+
+
+def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 10):
+    """The decode the way uplink runs it: every segment of a
+    download is rebuilt from whichever 29 pieces answered first
+    (private/eestream/stripe.go:314-354), so each brings a share set of its own
+    (ec_rebuild_segments_sets: the decode rows solved on the GPU, stream-ordered,
+    jump-table body).  Outside the timed region, informational:
+      * "32 segments, 32 fresh seeded 29-subsets per launch": HIP-event time per
+        call, calls back to back, and its HBM fraction (2 x S_pad per segment);
+      * "one segment, fresh set": wall clock per call, launch to synchronised
+        (median), and the stream time of such calls back to back."""
+    rng = np.random.default_rng(3229)
+    segs = torch.randint(0, 256, (nb, S_PAD), dtype=torch.uint8, device=dev)
+    pcs = torch.empty((nb, N, PIECE), dtype=torch.uint8, device=dev)
+    outs = torch.empty_like(segs)
+    stream = torch.cuda.current_stream(dev)
+    if L.ec_encode_segments(ctx, segs.data_ptr(), nb, NSTRIPES, pcs.data_ptr(), 0, sptr):
+        raise RuntimeError("encode failed")
+
+    def fresh(count):
+        return [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(count)]
+
+    def call(sets):
+        n = len(sets)
+        flat = [x for st in sets for x in st]
+        rc = L.ec_rebuild_segments_sets(
+            ctx, n, (ctypes.c_int * n)(*[K] * n), (ctypes.c_int * len(flat))(*flat),
+            (ctypes.c_void_p * len(flat))(*[pcs[g].data_ptr() + x * PIECE for g, st in enumerate(sets) for x in st]),
+            NSTRIPES, (ctypes.c_void_p * n)(*[outs[g].data_ptr() for g in range(n)]), sptr)
+        if rc:
+            raise RuntimeError(_native.strerror(rc))
+    outs.zero_()
+    call(fresh(nb))
+    torch.cuda.synchronize(dev)
+    ok = bool(torch.equal(outs, segs))
+    t_end = time.perf_counter() + 0.2  # clock settle
+    while time.perf_counter() < t_end:
+        call(fresh(nb))
+    all_sets = [fresh(nb) for _ in range(reps)]
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record(stream)
+    for i in range(reps):
+        call(all_sets[i])
+        ev[i + 1].record(stream)
+    ev[-1].synchronize()
+    per = [ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(reps)]
+    t = float(np.median(per))
+    ms = sorted(sum(1 for x in st if x >= K) for st in all_sets[0])
+    batch = {"us_per_launch": round(t * 1e6, 1), "us_per_segment": round(t / nb * 1e6, 2),
+             "GBps": round(2 * S_PAD * nb / t / 1e9, 1), "frac": round(2 * S_PAD * nb / t / 1e9 / HBM_PEAK_GBPS, 4),
+             "rows_per_segment": f"{ms[0]}..{ms[-1]} (median {ms[len(ms) // 2]})", "verified": ok}
+    walls = []
+    for _ in range(4 * reps):
+        one = fresh(1)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        call(one)
+        torch.cuda.synchronize(dev)
+        walls.append(time.perf_counter() - t0)
+    singles = [fresh(1) for _ in range(reps)]
+    torch.cuda.synchronize(dev)
+    e2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e2[0].record(stream)
+    for one in singles:
+        call(one)
+    e2[1].record(stream)
+    e2[1].synchronize()
+    b2b = e2[0].elapsed_time(e2[1]) * 1e-3 / reps
+    single = {"wall_us_median": round(float(np.median(walls)) * 1e6, 1), "wall_us_min": round(min(walls) * 1e6, 1),
+              "stream_us_back_to_back": round(b2b * 1e6, 1),
+              "frac_back_to_back": round(2 * S_PAD / b2b / 1e9 / HBM_PEAK_GBPS, 4)}
+    del segs, pcs, outs
+    return {f"{nb} segments, {nb} fresh seeded 29-subsets per launch": batch, "one segment, fresh set": single,
+            "note": "ec_rebuild_segments_sets; outside the timed region, informational, not in value"}
 
 
 def main():
@@ -481,6 +560,9 @@ def main():
         for i in range(len(sets)):
             encode(slot, B)
             decode(slot, B, i)
+    if hasattr(L, "ec_prepare_rebuild"):  # the sets' generated code, made in the background, ready before timing
+        for st in sets:
+            L.ec_prepare_rebuild(ctx, K, (ctypes.c_int * K)(*st), 1)
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < args.settle_s:
         for slot in range(pool):
@@ -671,13 +753,20 @@ def main():
         "build_id": L.ec_build_id().decode(),
         "verified": verified,
     }
-    if rank == 0 and world == 1 and not args.no_other_configs:
+    # after the timed region, on rank 0 at every world size: the decode with a
+    # fresh share set per segment, the reference benchmark's other configurations, the CPU baseline
+    if rank == 0 and hasattr(L, "ec_rebuild_segments_sets"):  # (an older --lib build lacks it)
+        line["fresh_share_sets"] = fresh_sets_leg(L, ctx, dev, sptr)
+    if rank == 0 and not args.no_other_configs:
         line["other_configs"] = other_configs(L, dev, sptr)
         line["other_configs"]["RS(29,80) rebuild, a new share set every launch"] = fresh_share_sets(L, dev, sptr)
-        if hasattr(L, "ec_decode_segments_batched"):  # (an older --lib build lacks it)
+        if hasattr(L, "ec_decode_segments_batched"):
             line["other_configs"]["RS(29,80) decode with error detection"] = decode_with_detection(L, dev, sptr)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample_s)
+    if use_dist:  # the other ranks wait for rank 0's informational legs
+        import torch.distributed as dist
+        dist.barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
     L.ec_destroy(ctx)

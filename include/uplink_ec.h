@@ -25,6 +25,8 @@
  *                            by single.go:228-238 (pieceReader.PieceReader)
  *   ec_rebuild_segments      batch form of the per-stripe Rebuild loop of
  *                            StripeReader.ReadStripes  stripe.go:382-428
+ *   ec_*_segments_sets       the same for many segments with a share set each:
+ *                            one StripeReader per download, ecclient/client.go:273-308
  *   ec_*_segments_host       the same batches from/to host memory (PCIe pipeline)
  *   ec_*blake3* / ec_hash_segments / ec_encode_segments_host_hashed
  *                            BLAKE3 piece hash of the upload (piecestore/upload.go:
@@ -74,6 +76,7 @@ extern "C" {
 
 /* flags for ec_encode_segments */
 #define EC_FLAG_PARITY_ONLY 0x1 /* write only the n-k parity pieces */
+#define EC_FLAG_HASH_PIECES 0x2 /* ec_upload_begin: also the BLAKE3 of every piece (ec_upload_hashes) */
 
 typedef struct ec_ctx ec_ctx;
 typedef void *ec_stream; /* hipStream_t; NULL = the default stream */
@@ -139,7 +142,10 @@ int ec_rebuild_segments_batched(const ec_ctx *ctx, int nshares, const int *nums,
  * segment with errors is then corrected and rebuilt again on its own.  Returns
  * when done (the check's outcome is read back), also when nshares == k:
  * EC_ERR_TOO_MANY_ERRORS / EC_ERR_NOT_ENOUGH_SHARES as Decode returns them.
- * Of more than 128 shares (n > 128), the first 128 in number order are used. */
+ * Every share given is checked and corrected, as infectious' Correct uses
+ * them all: of more than 128 (n > 128), the first 128 in number order go
+ * through the one-pass check and the syndromes of the rest are checked in
+ * further launches of up to 128 - k at a time. */
 int ec_decode_segments(const ec_ctx *ctx, int nshares, const int *nums, uint8_t *const *pieces, size_t nstripes,
                        uint8_t *out, ec_stream stream);
 /* The same over nseg segments in one check and one rebuild launch (strides as
@@ -147,6 +153,39 @@ int ec_decode_segments(const ec_ctx *ctx, int nshares, const int *nums, uint8_t 
 int ec_decode_segments_batched(const ec_ctx *ctx, int nshares, const int *nums, uint8_t *const *pieces,
                                size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
                                uint8_t *out, ec_stream stream);
+
+/* ---- a share set per segment (the download path as uplink runs it) ----
+ * Every segment a download fetches is decoded from whichever k (or more)
+ * pieces arrived first (StripeReader, private/eestream/stripe.go:314-354,
+ * via ecclient GetWithOptions, private/ecclient/client.go:273-308, one per
+ * segment, several at once under prefetch, private/storage/streams/
+ * store.go:240-253,385-403): share sets are almost never repeated.  These
+ * calls take nseg segments, each with its own set, in one pass: segment g's
+ * shares are entries [off_g, off_g + nshares[g]) of nums / pieces (off_g the
+ * sum of the nshares before it; device pointers, nstripes*ess bytes each, any
+ * order), its output outs[g] (nstripes*k*ess bytes, stripe-major).  The share
+ * choice is infectious Rebuild's per segment.  The decode rows of every
+ * segment are solved on the GPU in stream order; the host only chooses the
+ * shares (no synchronisation, no plan, no code generation on the call path).
+ *
+ * ec_rebuild_segments_sets: Rebuild (stripe.go:410-412); async on stream. */
+int ec_rebuild_segments_sets(const ec_ctx *ctx, size_t nseg, const int *nshares, const int *nums,
+                             const uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream);
+/* Decode with error detection (stripe.go:407-408 -> rs.go:32-38) over the
+ * same layout: one pass reads every share of every segment, stores the rebuilt
+ * data and checks each segment's syndromes; a segment with errors is then
+ * corrected in its pieces and rebuilt as ec_decode_segments does.  Returns
+ * when done.  Segments of more than 128 shares go through ec_decode_segments. */
+int ec_decode_segments_sets(const ec_ctx *ctx, size_t nseg, const int *nshares, const int *nums,
+                            uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream);
+/* ec_rebuild_segments[_batched] with a share set the context has no
+ * straight-line code for runs the share-set pass and has the code made in the
+ * background (DESIGN.md §4 "Straight-line rebuild bodies"); later launches of
+ * the set use it.  This queues that for (nshares, nums) ahead of time; with
+ * wait != 0 it returns after it is made.  Returns 1 when the code is ready, 0
+ * when not (or the set has none: every data share present).  No reference
+ * counterpart (an engine knob). */
+int ec_prepare_rebuild(const ec_ctx *ctx, int nshares, const int *nums, int wait);
 
 /* ---- host-memory pipeline (end-to-end path, PCIe-inclusive) ----
  * Same layouts as the device calls, but in host memory (pinned memory from
@@ -177,12 +216,22 @@ int ec_encode_segments_host_hashed(const ec_ctx *ctx, const uint8_t *segs, size_
  * ec_upload_wait blocks until stripes [0, stripes) of every piece are in host
  * memory; ec_upload_ready returns how many leading stripes are, without
  * blocking; ec_upload_end waits for the rest, frees the handle and returns the
- * first error.  The caller keeps seg and pieces alive until ec_upload_end. */
+ * first error.  The caller keeps seg and pieces alive until ec_upload_end.
+ * With EC_FLAG_HASH_PIECES the BLAKE3-256 of all n pieces (also with
+ * EC_FLAG_PARITY_ONLY) is computed as the chunks stream, as piecestore's
+ * upload hashes each piece through a TeeReader (piecestore/upload.go:155,
+ * 262-270); ec_upload_hashes waits for them (the last chunk's tree fold) and
+ * copies n*32 bytes into `hashes`.  Any number of threads may be inside
+ * ec_upload_wait / _ready / _hashes at once; ec_upload_end waits for those
+ * inside to return before it frees the handle, and no call may start on a
+ * handle once ec_upload_end has been called (callers arriving while it waits
+ * get EC_ERR_INVALID_ARG / 0). */
 typedef struct ec_upload ec_upload;
 int ec_upload_begin(const ec_ctx *ctx, const uint8_t *seg, size_t nstripes, uint8_t *pieces, int flags,
                     size_t chunk_stripes, ec_upload **out);
 int ec_upload_wait(ec_upload *u, size_t stripes);
 size_t ec_upload_ready(ec_upload *u);
+int ec_upload_hashes(ec_upload *u, uint8_t *hashes);
 int ec_upload_end(ec_upload *u);
 void *ec_host_alloc(size_t bytes); /* pinned (hipHostMalloc); NULL on failure */
 void ec_host_free(void *p);

@@ -53,6 +53,13 @@ def gpu_rebuild(sch, d_pieces, nums, stripes, nseg=1):
     return out.cpu().numpy()
 
 
+def prepare_code(sch, nums):
+    """Have the share set's straight-line code made now (the batched rebuild
+    otherwise makes it in the background after the set's first launch)."""
+    arr = (ctypes.c_int * len(nums))(*nums)
+    return sch._lib.ec_prepare_rebuild(sch._ctx, len(nums), arr, 1)
+
+
 def test_golden_fixtures_on_gpu():
     with open(os.path.join(HERE, "golden", "manifest.json")) as fh:
         man = json.load(fh)
@@ -109,8 +116,11 @@ def test_full_size_rs_29_80_64mib(oracle):
     for body in (_native.EC_BODY_AUTO, _native.EC_BODY_JUMP_TABLE):
         assert sch._lib.ec_set_body(sch._ctx, body) == 0
         for nums in (list(range(51, 80)), sorted(np.random.default_rng(29).choice(80, 29, replace=False).tolist())):
-            # EC_BODY_AUTO: a plan's first launch on the jump table, its second on generated code
+            # EC_BODY_AUTO: a share set's first launch on the jump table (the share-set pass), the
+            # next ones on generated code once it is made (here: waited for)
             for use in range(2 if body == _native.EC_BODY_AUTO else 1):
+                if use == 1:
+                    assert prepare_code(sch, nums) == 1
                 out = gpu_rebuild(sch, d_pieces, nums, 9040)[0]
                 assert np.array_equal(out, seg)
                 assert eestream.unpad(out.tobytes()) == raw.tobytes()
@@ -611,6 +621,7 @@ def test_auto_body_uses_straight_line_for_segments(oracle):
     nums = list(range(n - k, n))
     assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg)
     assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_JUMP_TABLE
+    assert prepare_code(sch, nums) == 1  # (queued by the first launch, made in the background)
     assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg)
     assert sch._lib.ec_last_body(sch._ctx) == _native.EC_BODY_STRAIGHT_LINE
     assert np.array_equal(gpu_rebuild(sch, d_pieces[:, :, :ess].contiguous(), nums, 1)[0], seg[:k * ess])
@@ -947,9 +958,10 @@ def test_decode_segments_batched(oracle):
 
 def test_auto_body_fresh_share_sets_recycle_plan_memory(oracle):
     """EC_BODY_AUTO with a new share set per call, past the 64 cached plans:
-    each set's first launch on the jump table, its second on generated code;
-    evicted plans return their tables to the context's arena, and the
-    recycled memory serves the next plans (every result checked)."""
+    each set's first launch on the jump table (share-set pass), the next on
+    generated code once the background builder has made it; evicted plans
+    return their tables to the context's arena, and the recycled memory serves
+    the next plans (every result checked)."""
     k, n, ess, stripes = 5, 12, 256, 512
     sch = scheme(k, n, ess)
     rng = np.random.default_rng(92)
@@ -960,6 +972,8 @@ def test_auto_body_fresh_share_sets_recycle_plan_memory(oracle):
     rng.shuffle(sets)
     for nums in sets[:150]:
         for want in (_native.EC_BODY_JUMP_TABLE, _native.EC_BODY_STRAIGHT_LINE):
+            if want == _native.EC_BODY_STRAIGHT_LINE:
+                assert prepare_code(sch, nums) == 1
             assert np.array_equal(gpu_rebuild(sch, d_pieces, nums, stripes)[0], seg), nums
             assert sch._lib.ec_last_body(sch._ctx) == want
 
@@ -1067,21 +1081,65 @@ def test_decode_segments_fused_pass_every_shape(oracle, body):
 
 
 def test_decode_segments_wide_code_more_than_128_shares(oracle):
-    """Decode of a wide code given more than 128 shares uses the
-    first 128 in number order (a launch takes at most 128 inputs) instead of
-    failing: RS(100,200) from 150 shares, clean and with one corrupted piece
-    among the first 128."""
-    k, n, ess, stripes = 100, 200, 256, 24
+    """Decode of a wide code given more than 128 shares
+    checks and corrects every share, as infectious' Correct does
+    (private/eestream/rs.go:32-38): RS(100,200) from all 200 shares --
+      * clean;
+      * one corrupted share past the 128th (outside the one-pass launch's
+        inputs: caught by the further syndrome launches, corrected in place);
+      * 30 corrupted shares (e = 50 over 200 shares corrects them; over the
+        first 128 alone, e = 14 could not);
+      * scattered errors in a few columns of many shares;
+    every output and every corrected share against the oracle (its Decode and
+    its encode), and 51 bad shares: TooManyErrors."""
+    k, n, ess, stripes = 100, 200, 256, 8
     sch = scheme(k, n, ess)
-    rng = np.random.default_rng(150)
+    rng = np.random.default_rng(200)
     seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
-    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
-    nums = [int(x) for x in rng.permutation(n)[:150]]
+    f = oracle.FEC(k, n)
+    ref = f.encode_segment(seg, ess, threads=8)
+    nums = [int(x) for x in rng.permutation(n)]
     d_pieces = torch.from_numpy(ref).cuda().reshape(1, n, -1)
     assert np.array_equal(gpu_decode_segments(sch, d_pieces, nums, stripes), seg)
-    recv = ref.copy()
-    bad = sorted(nums)[5]
-    recv[bad] ^= rng.integers(1, 256, stripes * ess, dtype=np.uint8)
+    srt = sorted(nums)
+
+    def corrupt(bad, cols=None):
+        recv = ref.copy()
+        for i, b in enumerate(bad):
+            if cols is None:
+                recv[b] ^= rng.integers(1, 256, stripes * ess, dtype=np.uint8)
+            else:
+                recv[b, cols[i % len(cols)]] ^= 0x3C
+        return recv
+    for bad, cols in (([srt[150]], None), (sorted(rng.choice(n, 30, replace=False).tolist()), None),
+                      (srt[::7], [3, 700, 1500])):
+        recv = corrupt(bad, cols)
+        # the oracle's Decode of the same shares, stripe by stripe (infectious' Correct + Rebuild)
+        want = np.concatenate([f.decode(nums, [recv[x, s * ess:(s + 1) * ess] for x in nums]) for s in range(stripes)])
+        assert np.array_equal(want, seg)
+        d_bad = torch.from_numpy(recv).cuda().reshape(1, n, -1)
+        assert np.array_equal(gpu_decode_segments(sch, d_bad, nums, stripes), want), bad[:4]
+        assert np.array_equal(d_bad.cpu().numpy()[0], ref), bad[:4]  # every bad share corrected in place
+    recv = corrupt(sorted(rng.choice(n, 51, replace=False).tolist()))
     d_bad = torch.from_numpy(recv).cuda().reshape(1, n, -1)
-    assert np.array_equal(gpu_decode_segments(sch, d_bad, nums, stripes), seg)
-    assert np.array_equal(d_bad.cpu().numpy()[0][bad], ref[bad])
+    with pytest.raises(Exception, match="too many errors"):
+        gpu_decode_segments(sch, d_bad, nums, stripes)
+
+
+def test_decode_host_wide_code_all_shares(oracle):
+    """ec_decode (the per-stripe ErasureScheme.Decode) of a wide code: 200
+    shares, 40 of them bad, corrected in place against the oracle."""
+    k, n, ess = 100, 200, 64
+    sch = scheme(k, n, ess)
+    rng = np.random.default_rng(201)
+    stripe = rng.integers(0, 256, k * ess, dtype=np.uint8)
+    f = oracle.FEC(k, n)
+    allsh = f.encode(stripe)
+    bad = sorted(rng.choice(n, 40, replace=False).tolist())
+    shares = [eestream.Share(i, np.array(allsh[i])) for i in range(n)]
+    for b in bad:
+        shares[b].data[rng.integers(0, ess)] ^= 0x77
+    out = sch.decode(None, shares)
+    assert np.array_equal(out, stripe)
+    for sh in shares:
+        assert np.array_equal(sh.data, allsh[sh.number]), sh.number

@@ -72,6 +72,7 @@ def test_two_rank_gloo_sharded_encode(oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
 def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
     """The bench's N > 1 path with the HIP engine: two ranks (torch
     distributed run) share the box's one GPU and use gloo for the barrier and
@@ -89,7 +90,8 @@ def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
     env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
-           "2", "--warmup", "1", "--settle-s", "0", "--total-segments", "64", "--no-cpu-baseline"]
+           "2", "--warmup", "1", "--settle-s", "0", "--total-segments", "64", "--cpu-sample-s", "0.5",
+           "--no-other-configs"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -100,6 +102,11 @@ def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
     assert line["ranks_seen"] == 2
     assert len(line["rank_wall_s"]) == 2 and all(w > 0 for w in line["rank_wall_s"])
     assert line["ms_per_step"] == pytest.approx(max(line["rank_wall_s"]) / line["steps"] * 1e3, rel=1e-3)
+    # the N > 1 line carries the same-run CPU baseline and the fresh-share-set decode leg
+    assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["cores"] >= 1
+    fs = line["fresh_share_sets"]
+    assert fs["32 segments, 32 fresh seeded 29-subsets per launch"]["verified"] is True
+    assert fs["one segment, fresh set"]["wall_us_median"] > 0
 
 
 @pytest.mark.gpu

@@ -139,6 +139,8 @@ def test_streamed_parity_pieces_read_in_small_reads(oracle, chunk):
     for num in readers:
         assert b"".join(got[num]) == ref[num].tobytes(), num
     assert spr.ready_stripes() == plen // ess
+    for r in readers.values():
+        r.close()
     spr.close()
     with pytest.raises(eestream.EEStreamError):
         spr._wait(1)
@@ -181,3 +183,149 @@ def test_streamed_upload_c_abi_partial_wait_and_threads(oracle):
         assert lib.ec_upload_end(h) == 0
         assert np.array_equal(view, ref[n - rows:])
         pieces.close()
+
+
+@pytest.mark.parametrize("k,n,ess,size,chunk", [
+    (29, 80, 256, 3 * 1024 * 1024 + 123, 0),    # the library's chunks (128, 256, ... 2048 stripes)
+    (29, 80, 256, 2 * 1024 * 1024 + 5, 300),    # 300 stripes = 75 BLAKE3 chunks per piece chunk
+    (29, 80, 256, 1024 * 1024, 7),              # 7 stripes: not whole BLAKE3 chunks -> hashed after the last
+    (4, 10, 256, 1 << 20, 4),                   # 4 stripes = 1 KiB per chunk
+    (20, 60, 4096, 5 * 81920 - 4, 0), (29, 80, 256, 100, 0),  # pieces of one BLAKE3 chunk: after the last
+])
+def test_streamed_upload_hashes_pieces(oracle, k, n, ess, size, chunk):
+    """SegmentPieceReader(hash_pieces=True) streams the
+    parity and hashes every piece chunk by chunk (EC_FLAG_HASH_PIECES), as the
+    reference hashes each piece through a TeeReader while it streams
+    (piecestore/upload.go:155,262-270).  Every piece's BLAKE3 against the
+    oracle's hash of the oracle's piece -- asked before any piece is read (it
+    waits only for the tree fold) -- and the piece bytes."""
+    from oracle import blake3 as ob
+    rs = _rs(k, n, ess)
+    data = np.random.default_rng(size + chunk).integers(0, 256, size, dtype=np.uint8).tobytes()
+    padded = eestream.pad(data, rs.stripe_size())
+    ref = oracle.FEC(k, n).encode_segment(np.frombuffer(padded, dtype=np.uint8), ess, threads=8)
+    want = ob.blake3_many(ref, threads=8)
+    spr = segment.SegmentPieceReader(data, rs, hash_pieces=True, chunk_stripes=chunk)
+    try:
+        for num in range(n):
+            assert spr.piece_hash(num) == want[num].tobytes(), num
+        for num in sorted({0, k - 1, k, n - 1}):
+            with _closing(spr.piece_reader(num)) as r:
+                assert r.read() == ref[num].tobytes(), num
+    finally:
+        spr.close()
+
+
+class _closing:
+    def __init__(self, r):
+        self.r = r
+
+    def __enter__(self):
+        return self.r
+
+    def __exit__(self, *a):
+        self.r.close()
+
+
+def test_upload_hashes_c_abi(oracle):
+    """ec_upload_begin(EC_FLAG_HASH_PIECES): all n hashes for the full layout
+    and the parity-only one; ec_upload_hashes on an upload begun without the
+    flag is an argument error; unknown flags are refused."""
+    import ctypes
+    from oracle import blake3 as ob
+    from uplink_amd import _native as NAT
+    lib = NAT.load()
+    k, n, ess, stripes = 29, 80, 256, 2100
+    sch = eestream.RSScheme(eestream.new_fec(k, n), ess)
+    seg = np.random.default_rng(21).integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    want = ob.blake3_many(ref, threads=8)
+    assert lib.ec_upload_begin(sch.ctx, seg.ctypes.data, stripes, seg.ctypes.data, 0x80, 0,
+                               ctypes.byref(ctypes.c_void_p())) == NAT.EC_ERR_INVALID_ARG
+    for flags, rows in ((NAT.EC_FLAG_HASH_PIECES, n), (NAT.EC_FLAG_HASH_PIECES | NAT.EC_FLAG_PARITY_ONLY, n - k),
+                        (NAT.EC_FLAG_PARITY_ONLY, n - k)):
+        pieces = segment.PinnedHost(rows * stripes * ess)
+        h = ctypes.c_void_p()
+        assert lib.ec_upload_begin(sch.ctx, seg.ctypes.data, stripes, pieces.ptr, flags, 0, ctypes.byref(h)) == 0
+        hashes = np.zeros((n, 32), dtype=np.uint8)
+        rc = lib.ec_upload_hashes(h, hashes.ctypes.data)
+        if flags & NAT.EC_FLAG_HASH_PIECES:
+            assert rc == 0 and np.array_equal(hashes, want), flags
+        else:
+            assert rc == NAT.EC_ERR_INVALID_ARG
+        assert lib.ec_upload_end(h) == 0
+        assert np.array_equal(pieces.array.reshape(rows, -1), ref[n - rows:])
+        pieces.close()
+
+
+def test_piece_stream_keeps_buffers_after_reader_close(oracle):
+    """a piece stream still being read keeps the reader's
+    pinned buffers; closing (or dropping) the reader hands them back to the
+    pool only after its last stream closes.  Another segment's reader, taking
+    buffers of the same size from the pool meanwhile, must not change what the
+    first reader's open streams return."""
+    import gc
+    k, n, ess = 29, 80, 256
+    rs = _rs(k, n, ess)
+    size = 1024 * 1024
+    rng = np.random.default_rng(31)
+    d1, d2 = (rng.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(2))
+    ref1 = oracle.FEC(k, n).encode_segment(np.frombuffer(eestream.pad(d1, rs.stripe_size()), dtype=np.uint8), ess)
+    a = segment.SegmentPieceReader(d1, rs)
+    data_stream, parity_stream = a.piece_reader(3), a.piece_reader(40)
+    first = data_stream.read(1000)
+    a.close()  # streams open: the buffers stay with them
+    with pytest.raises(eestream.EEStreamError):
+        a.piece_reader(4)
+    b = segment.SegmentPieceReader(d2, rs)  # same sizes: would take the pool's buffers
+    assert len(b.piece_reader(40).read()) > 0 and len(b.piece_reader(3).read()) > 0
+    assert first + data_stream.read() == ref1[3].tobytes()
+    assert parity_stream.read() == ref1[40].tobytes()
+    data_stream.close()
+    parity_stream.close()  # the last one: a's buffers go back now
+    b.close()
+    # dropping a reader whose streams are alive: the streams hold it, nothing is released under them
+    c = segment.SegmentPieceReader(d1, rs)
+    s3 = c.piece_reader(3)
+    del c
+    gc.collect()
+    d = segment.SegmentPieceReader(d2, rs)
+    d.piece_reader(3).read()
+    assert s3.read() == ref1[3].tobytes()
+    s3.close()
+    d.close()
+
+
+def test_upload_end_waits_for_callers_inside():
+    """ec_upload_end while other threads are inside
+    ec_upload_wait / _ready on the same handle returns only after they have
+    left (no use of the freed handle)."""
+    import ctypes
+    import threading
+    import time
+    from uplink_amd import _native as NAT
+    lib = NAT.load()
+    k, n, ess, stripes = 29, 80, 256, 9040
+    sch = eestream.RSScheme(eestream.new_fec(k, n), ess)
+    seg = segment.PinnedHost(stripes * k * ess)
+    seg.array[:] = 7
+    pieces = segment.PinnedHost((n - k) * stripes * ess)
+    for rep in range(3):
+        h = ctypes.c_void_p()
+        assert lib.ec_upload_begin(sch.ctx, seg.ptr, stripes, pieces.ptr, NAT.EC_FLAG_PARITY_ONLY, 0,
+                                   ctypes.byref(h)) == 0
+        go = threading.Barrier(9)
+        rcs = []
+
+        def waiter(t):
+            go.wait()
+            rcs.append(lib.ec_upload_wait(h, stripes) if t % 2 else int(lib.ec_upload_ready(h) >= 0))
+        th = [threading.Thread(target=waiter, args=(t,)) for t in range(8)]
+        [t.start() for t in th]
+        go.wait()
+        time.sleep(0.02)  # the waiters are inside their calls
+        assert lib.ec_upload_end(h) == 0
+        [t.join() for t in th]
+        assert all(r in (0, 1, NAT.EC_ERR_INVALID_ARG) for r in rcs), rcs
+    seg.close()
+    pieces.close()

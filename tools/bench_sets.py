@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Fresh share sets, the way uplink decodes: every
+segment of a download comes with whichever 29 pieces answered first
+(private/eestream/stripe.go:314-354), so its decode plan is new.
+
+  * batch: ec_rebuild_segments_sets, 32 RS(29,80) 64 MiB segments per call,
+    32 fresh seeded 29-subsets per call; HIP-event time per call on the
+    stream (launches back to back) and wall time per call.
+  * single: one segment, a fresh set, wall clock per call (launch + sync).
+  * batched API (ec_rebuild_segments_batched) on a fresh set: first, second
+    and warm launch of the set, wall clock, one segment and 16.
+Run on the GPU box: python tools/bench_sets.py [--reps N]"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from uplink_amd import _native  # noqa: E402
+
+K, N, ESS = 29, 80, 256
+NSTRIPES = (64 * 2**20 + 4 + K * ESS - 1) // (K * ESS)
+SPAD, PLEN = NSTRIPES * K * ESS, NSTRIPES * ESS
+PEAK = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=12)
+    ap.add_argument("--nseg", type=int, default=32)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    L = _native.load()
+    ctx = ctypes.c_void_p()
+    assert L.ec_create(K, N, ESS, ctypes.byref(ctx)) == 0
+    dev = torch.device("cuda", 0)
+    nseg = args.nseg
+    segs = torch.randint(0, 256, (nseg, SPAD), dtype=torch.uint8, device=dev)
+    pcs = torch.empty((nseg, N, PLEN), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    sptr = st.cuda_stream
+    assert L.ec_encode_segments(ctx, segs.data_ptr(), nseg, NSTRIPES, pcs.data_ptr(), 0, sptr) == 0
+    outs = torch.empty_like(segs)
+    rng = np.random.default_rng(2905)
+
+    def fresh(count):
+        return [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(count)]
+
+    def sets_call(sets, out=outs):
+        n = len(sets)
+        nsh = (ctypes.c_int * n)(*[K] * n)
+        flat = [x for s in sets for x in s]
+        nums = (ctypes.c_int * len(flat))(*flat)
+        ptrs = (ctypes.c_void_p * len(flat))(*[pcs[g].data_ptr() + x * PLEN for g, s in enumerate(sets) for x in s])
+        optr = (ctypes.c_void_p * n)(*[out[g].data_ptr() for g in range(n)])
+        rc = L.ec_rebuild_segments_sets(ctx, n, nsh, nums, ptrs, NSTRIPES, optr, sptr)
+        assert rc == 0, _native.strerror(rc)
+
+    res = {}
+    # warm-up (kernels loaded, slots allocated)
+    for _ in range(3):
+        sets_call(fresh(nseg))
+    torch.cuda.synchronize()
+    outs.zero_()
+    sets_call(fresh(nseg))
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(outs, segs))
+    # batch: back to back, events around each call
+    t_end = time.perf_counter() + 0.3
+    while time.perf_counter() < t_end:  # clock settle
+        sets_call(fresh(nseg))
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
+    all_sets = [fresh(nseg) for _ in range(args.reps)]
+    ev[0].record(st)
+    t0 = time.perf_counter()
+    for i in range(args.reps):
+        sets_call(all_sets[i])
+        ev[i + 1].record(st)
+    ev[-1].synchronize()
+    wall = (time.perf_counter() - t0) / args.reps
+    per = [ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(args.reps)]
+    t = float(np.median(per))
+    alg = nseg * 2 * SPAD
+    res["batch"] = {"segments_per_call": nseg, "us_per_call_median": round(t * 1e6, 1),
+                    "us_per_call_mean": round(float(np.mean(per)) * 1e6, 1),
+                    "us_per_segment": round(t / nseg * 1e6, 2), "GBps": round(alg / t / 1e9, 1),
+                    "frac": round(alg / t / 1e9 / PEAK, 4), "wall_us_per_call": round(wall * 1e6, 1),
+                    "m_of_sets": sorted(int(sum(1 for x in s if x >= K)) for s in all_sets[0])}
+    # single segment, fresh set, synchronous wall clock
+    walls = []
+    for i in range(args.reps * 4):
+        s1 = fresh(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sets_call(s1, outs)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+    ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    s1s = [fresh(1) for _ in range(args.reps)]
+    torch.cuda.synchronize()
+    ev2[0].record(st)
+    for s1 in s1s:
+        sets_call(s1, outs)
+    ev2[1].record(st)
+    ev2[1].synchronize()
+    b2b = ev2[0].elapsed_time(ev2[1]) * 1e-3 / args.reps
+    res["single"] = {"wall_us_median": round(float(np.median(walls)) * 1e6, 1),
+                     "wall_us_min": round(min(walls) * 1e6, 1),
+                     "stream_us_back_to_back": round(b2b * 1e6, 1),
+                     "frac_back_to_back": round(2 * SPAD / b2b / 1e9 / PEAK, 4)}
+    # the batched single-set API on fresh sets: first / second / warm, wall clock
+    for n in (1, 16):
+        rows = []
+        for i in range(args.reps):
+            nums = fresh(1)[0]
+            cn = (ctypes.c_int * K)(*nums)
+            cp = (ctypes.c_void_p * K)(*[pcs[0].data_ptr() + x * PLEN for x in nums])
+            t = []
+            for rep in range(3):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                assert L.ec_rebuild_segments_batched(ctx, K, cn, cp, NSTRIPES, n, N * PLEN, SPAD, outs.data_ptr(),
+                                                     sptr) == 0
+                torch.cuda.synchronize()
+                t.append(time.perf_counter() - t0)
+                if rep == 1:
+                    L.ec_prepare_rebuild(ctx, K, cn, 1)
+            rows.append(t)
+        a = np.array(rows) * 1e6
+        res[f"batched_api_{n}seg"] = {"first_us": round(float(np.median(a[:, 0])), 1),
+                                      "second_us": round(float(np.median(a[:, 1])), 1),
+                                      "warm_us": round(float(np.median(a[:, 2])), 1),
+                                      "second_max_us": round(float(a[:, 1].max()), 1)}
+    res["verified"] = ok
+    print(json.dumps(res))
+    L.ec_destroy(ctx)
+
+
+if __name__ == "__main__":
+    main()

@@ -29,6 +29,7 @@ EC_ERR_SHARE_SIZE = -13
 EC_ERR_AUTH = -14
 
 EC_FLAG_PARITY_ONLY = 0x1
+EC_FLAG_HASH_PIECES = 0x2
 # ec_set_body: body of the runtime-matrix kernel (include/uplink_ec.h)
 EC_BODY_AUTO, EC_BODY_JUMP_TABLE, EC_BODY_STRAIGHT_LINE = 0, 1, 2
 
@@ -63,6 +64,13 @@ SIGNATURES = {
     "ec_rebuild_segments_batched": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_size_t,
                                                    ctypes.c_longlong, ctypes.c_longlong, vp, vp]),
+    "ec_rebuild_segments_sets": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp), ctypes.c_size_t,
+                                                ctypes.POINTER(vp), vp]),
+    "ec_decode_segments_sets": (ctypes.c_int, [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
+                                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp), ctypes.c_size_t,
+                                               ctypes.POINTER(vp), vp]),
+    "ec_prepare_rebuild": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "ec_encode_segments_host": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, ctypes.c_int]),
     "ec_rebuild_segments_host": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
                                                 ctypes.c_size_t, ctypes.c_size_t, ctypes.c_longlong, vp]),
@@ -89,6 +97,7 @@ SIGNATURES = {
                                        ctypes.POINTER(vp)]),
     "ec_upload_wait": (ctypes.c_int, [vp, ctypes.c_size_t]),
     "ec_upload_ready": (ctypes.c_size_t, [vp]),
+    "ec_upload_hashes": (ctypes.c_int, [vp, vp]),
     "ec_upload_end": (ctypes.c_int, [vp]),
     "ec_host_alloc": (vp, [ctypes.c_size_t]),
     "ec_host_free": (None, [vp]),

@@ -222,6 +222,27 @@ __global__ __launch_bounds__(kGroup) void b3_parents(const uint32_t *nodes_in, u
     }
 }
 
+// Streamed hashing (ec_upload with EC_FLAG_HASH_PIECES): the CVs of chunks
+// [c0, c1) of every piece, written to cvs[piece][c][8] of pieces of nchunks
+// >= 2 chunks (so no chunk is the root), one lane per chunk.  Once every range
+// is in, b3_parents folds cvs level by level exactly as b3_chunks folds a
+// group (pairs, an odd last node moving up).
+template <bool kFast>
+__global__ __launch_bounds__(kGroup) void b3_chunk_range(B3Pair pv, uint64_t c0, uint64_t c1, uint32_t groups,
+                                                         uint64_t nchunks, uint32_t *cvs) {
+    const uint64_t piece = blockIdx.x / groups;
+    const uint64_t c = c0 + (uint64_t)(blockIdx.x % groups) * kGroup + threadIdx.x;
+    if (c >= c1) return;
+    const bool second = piece >= pv.split;
+    const B3View &v = pv.v[second];
+    const uint8_t *pb = piece_base(v, second ? piece - pv.split : piece);
+    uint32_t h[8];
+    chunk_cv<kFast>(v, pb, c, false, h);
+    uint4 *o = reinterpret_cast<uint4 *>(cvs + (piece * nchunks + c) * 8);
+    o[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    o[1] = make_uint4(h[4], h[5], h[6], h[7]);
+}
+
 uint64_t chunks_of(const B3View &v) { return v.piece_len ? (v.piece_len + 1023) / 1024 : 1; }
 uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
@@ -274,6 +295,47 @@ hipError_t b3_launch2(const B3View &first, const B3View &second, uint8_t *hashes
     hipError_t e = hipGetLastError();
     while (e == hipSuccess && groups > 1) {
         const uint64_t next = ceil_div(groups, kGroup);
+        b3_parents<<<dim3((uint32_t)(npieces * next)), kGroup, 0, stream>>>(a, (uint32_t)groups, (uint32_t)next, b,
+                                                                          hashes);
+        e = hipGetLastError();
+        groups = next;
+        uint32_t *t = a;
+        a = b;
+        b = t;
+    }
+    return e;
+}
+
+hipError_t b3_launch_chunk_range(const B3View &first, const B3View &second, uint64_t c0, uint64_t c1, uint32_t *cvs,
+                                 hipStream_t stream) {
+    if (second.npieces && first.npieces && second.piece_len != first.piece_len) return hipErrorInvalidValue;
+    B3Pair pv{{normalized(first), normalized(second)}, first.npieces};
+    const uint64_t npieces = first.npieces + second.npieces;
+    const uint64_t nchunks = chunks_of(first.npieces ? first : second);
+    if (npieces == 0 || c1 <= c0) return hipSuccess;
+    if (nchunks < 2 || c1 > nchunks || !cvs) return hipErrorInvalidValue;
+    const uint64_t groups = ceil_div(c1 - c0, kGroup);
+    if (npieces * groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)(npieces * groups));
+    if (fast_ok(pv.v[0]) && fast_ok(pv.v[1]))
+        b3_chunk_range<true><<<grid, kGroup, 0, stream>>>(pv, c0, c1, (uint32_t)groups, nchunks, cvs);
+    else
+        b3_chunk_range<false><<<grid, kGroup, 0, stream>>>(pv, c0, c1, (uint32_t)groups, nchunks, cvs);
+    return hipGetLastError();
+}
+
+size_t b3_fold_ws_bytes(uint64_t npieces, uint64_t nchunks) { return (size_t)(npieces * ceil_div(nchunks, kGroup) * 32); }
+
+hipError_t b3_launch_fold(uint32_t *cvs, uint64_t npieces, uint64_t nchunks, uint8_t *hashes, void *ws,
+                          hipStream_t stream) {
+    if (npieces == 0) return hipSuccess;
+    if (nchunks < 2) return hipErrorInvalidValue;
+    uint32_t *a = cvs, *b = static_cast<uint32_t *>(ws);  // (after the first level, cvs is the scratch)
+    uint64_t groups = nchunks;
+    hipError_t e = hipSuccess;
+    while (e == hipSuccess && groups > 1) {
+        const uint64_t next = ceil_div(groups, kGroup);
+        if (npieces * next > 0x7FFFFFFFull) return hipErrorInvalidValue;
         b3_parents<<<dim3((uint32_t)(npieces * next)), kGroup, 0, stream>>>(a, (uint32_t)groups, (uint32_t)next, b,
                                                                           hashes);
         e = hipGetLastError();

@@ -35,5 +35,14 @@ hipError_t b3_launch(const B3View &v, uint8_t *hashes, void *ws, hipStream_t str
 // Both views in one launch (equal piece_len): hashes of `first`'s pieces,
 // then `second`'s.  ws: b3_workspace_bytes of a view with the summed npieces.
 hipError_t b3_launch2(const B3View &first, const B3View &second, uint8_t *hashes, void *ws, hipStream_t stream);
+// Streamed form (pieces of >= 2 chunks): the chaining values of BLAKE3 chunks
+// [c0, c1) of every piece of both views into cvs [npieces][nchunks][8 words],
+// as the bytes of those chunks become available; then b3_launch_fold turns the
+// complete cvs into the hashes (cvs is overwritten; ws: b3_fold_ws_bytes).
+hipError_t b3_launch_chunk_range(const B3View &first, const B3View &second, uint64_t c0, uint64_t c1, uint32_t *cvs,
+                                 hipStream_t stream);
+size_t b3_fold_ws_bytes(uint64_t npieces, uint64_t nchunks);
+hipError_t b3_launch_fold(uint32_t *cvs, uint64_t npieces, uint64_t nchunks, uint8_t *hashes, void *ws,
+                          hipStream_t stream);
 
 }  // namespace uplink_ec

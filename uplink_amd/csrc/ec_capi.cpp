@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -17,6 +18,8 @@
 #include <deque>
 #include <atomic>
 #include <mutex>
+#include <set>
+#include <thread>
 #include <vector>
 
 #include "../../include/uplink_ec.h"
@@ -24,6 +27,7 @@
 #include "gf256.hpp"
 #include "rs_correct.hpp"
 #include "rs_kernels.hpp"
+#include "rs_sets.hpp"
 #include "rs_sl.hpp"
 
 using namespace uplink_ec;
@@ -161,6 +165,7 @@ struct MatPlan {
     std::vector<uint8_t> M;        // rows x nin, row-major (for the straight-line code)
     std::mutex sl_mu;
     bool sl_tried = false;
+    std::atomic<bool> sl_ready{false};  // d_sl is set (launch paths read this, not d_sl, without sl_mu)
     hipModule_t sl_mod = nullptr;
     uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
     // The plan's launches, as (stream, sequence number) of the context's
@@ -249,13 +254,76 @@ struct HostPipe {
 };
 
 // Device side of one streamed upload (ec_upload_begin): the segment, its
-// pieces and the three role streams (H2D, encode, D2H).  Kept in a per-context
-// pool between uploads; one upload owns a slot from begin to end.
+// pieces and the four role streams (H2D, encode, D2H, piece hashes).  Kept in
+// a per-context pool between uploads; one upload owns a slot from begin to end.
 struct UploadSlot {
-    hipStream_t st[3] = {};
+    hipStream_t st[4] = {};
     uint8_t *d_in = nullptr, *d_out = nullptr;
     size_t in_cap = 0, out_cap = 0;
-    std::vector<hipEvent_t> ev;  // [in ch][enc ch][d2h ch] of the current upload
+    uint8_t *d_hash = nullptr;   // EC_FLAG_HASH_PIECES: chunk CVs | hashes | fold scratch
+    size_t hash_cap = 0;
+    uint8_t *h_hash = nullptr;   // pinned, n*32 bytes: the hashes as they come back
+    size_t h_hash_cap = 0;
+    std::vector<hipEvent_t> ev;  // [in ch][enc ch][d2h ch][hashes] of the current upload
+    ~UploadSlot() {  // (also on an error path of ec_upload_begin: nothing of it is left behind)
+        for (auto st : this->st)
+            if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
+        for (auto e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (d_in) (void)hipFree(d_in);
+        if (d_out) (void)hipFree(d_out);
+        if (d_hash) (void)hipFree(d_hash);
+        if (h_hash) (void)hipHostFree(h_hash);
+    }
+};
+
+// One slot of a context's share-set calls (rs_sets.hpp): the pinned staging
+// the host writes, the device descriptors and leaf tables rs_sets_prep makes
+// from it, and the words the launches report through.  A call takes a slot
+// whose previous call has finished on the GPU -- its last workgroup stores the
+// call's sequence number into *h_done (pinned) -- so neither the host's writes
+// nor the prep kernel's ever overtake a launch still reading the slot, and no
+// event, marker or synchronisation is put on the caller's stream.
+struct SetsSlot {
+    SetStage *h_stage = nullptr;  // pinned, stage_cap entries
+    size_t stage_cap = 0;
+    SetDesc *d_desc = nullptr;    // device, stage_cap entries
+    uint64_t *d_tgt = nullptr;    // device leaf tables, tgt_cap words
+    size_t tgt_cap = 0;
+    uint32_t *d_words = nullptr;  // device: [0] done counter, [1 + g] segment g's syndrome count (stage_cap + 1)
+    uint32_t *h_words = nullptr;  // pinned: [0] done sequence number, [1 + g] syndrome counts read back (Decode)
+    uint32_t seq = 0;             // of the slot's latest call
+    bool busy = false;            // a caller is filling or launching it
+    bool dead = false;            // a launch failed after the prep: never reused
+    ~SetsSlot() {
+        if (h_stage) (void)hipHostFree(h_stage);
+        if (d_desc) (void)hipFree(d_desc);
+        if (d_tgt) (void)hipFree(d_tgt);
+        if (d_words) (void)hipFree(d_words);
+        if (h_words) (void)hipHostFree(h_words);
+    }
+    bool idle() const { return !busy && !dead && __atomic_load_n(h_words, __ATOMIC_ACQUIRE) == seq; }
+};
+
+struct SetsRing {
+    static constexpr size_t kMaxSlots = 16;  // calls in flight per context before a caller waits
+    std::mutex mu;
+    std::vector<std::unique_ptr<SetsSlot>> slots;
+};
+
+// Background maker of decode plans' straight-line code (DESIGN.md §4
+// "Straight-line rebuild bodies"): code generation and hipModuleLoadData take
+// ~0.4 ms per share set, so a batched rebuild never waits for them.  A launch
+// whose share set has no ready code runs the share-set path (jump-table body,
+// rs_sets.hpp) and queues the set here; later launches of the set take the
+// generated code once it has landed.
+struct SlBuilder {
+    std::mutex mu;
+    std::condition_variable cv;      // work queued / stop (worker), a set finished (waiters)
+    std::deque<std::vector<int>> q;  // share sets (chosen ids) to build
+    std::set<std::vector<int>> pending;
+    std::thread th;
+    bool stop = false;
 };
 
 // Work counters of the compile-time encoder's launches (RsArgs::queue): a
@@ -314,6 +382,10 @@ struct ec_ctx {
     // at ec_create): EncodeSingle batches of more than M requests find no
     // staging, nor does a one-request batch for share J
     int fault_max_batch = 0, fault_fail_num = -1;
+    // share-set calls (ec_*_segments_sets, and fresh share sets of the batched rebuild)
+    uint64_t jt_base = 0;          // address of the jump table's leaf 0 on this device
+    SetsRing sets;
+    SlBuilder slb;
 };
 
 namespace {
@@ -692,6 +764,7 @@ void ensure_sl(ec_ctx *c, MatPlan &plan) {
     plan.sl_mod = mod;
     plan.d_sl = d;
     plan.sl_bytes = dbytes;
+    plan.sl_ready.store(true, std::memory_order_release);
 }
 
 // Launch the product described by `a` with the rows of `plan` (out_off gives
@@ -718,9 +791,10 @@ int run_matmul(ec_ctx *c, RsArgs a, const int64_t *out_off, MatPlan &plan, int64
         // ~0.9 ms against ~50 us of kernel time per segment)
         const bool want_sl = bitsliced && total_rows <= kMaxOps && c->body != EC_BODY_JUMP_TABLE &&
                              (c->body == EC_BODY_STRAIGHT_LINE ||
-                              (a.total_tiles >= kSlMinTiles && plan.launches.load() > 0));
+                              (a.total_tiles >= kSlMinTiles &&
+                               (plan.launches.load() > 0 || plan.sl_ready.load(std::memory_order_acquire))));
         if (want_sl) ensure_sl(c, plan);
-        if (want_sl && plan.d_sl) {
+        if (want_sl && plan.sl_ready.load(std::memory_order_acquire)) {
             a.jt_tgt = plan.d_sl;
             c->last_body = EC_BODY_STRAIGHT_LINE;
             HIP_TRY(launch_matmul_sl(a, 0, s));
@@ -783,18 +857,12 @@ int get_plan(ec_ctx *c, const std::vector<int> &ids, PlanPtr *out) {
     }, out);
 }
 
-// Core rebuild: device pointers of the nshares pieces, nstripes stripes of
-// share size `ess`, out stripe-major; batched over nseg with strides.
-int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int ess, int64_t nstripes,
-                   int64_t nseg, int64_t piece_seg_stride, int64_t out_seg_stride, uint8_t *out, hipStream_t s) {
-    std::vector<int> order, ids;
-    int rc = choose_shares(c, nshares, nums, order, ids);
-    if (rc) return rc;
+// The rebuild of nseg segments from the chosen shares (order: their indices in
+// `pieces`, ids: their numbers) with a decode plan.
+int rebuild_with_plan(ec_ctx *c, MatPlan &plan, const std::vector<int> &order, const std::vector<int> &ids,
+                      const uint8_t *const *pieces, int ess, int64_t nstripes, int64_t nseg, int64_t piece_seg_stride,
+                      int64_t out_seg_stride, uint8_t *out, hipStream_t s) {
     const int k = c->k;
-    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
-    PlanPtr plan;
-    rc = get_plan(c, ids, &plan);
-    if (rc) return rc;
     RsArgs a{};
     const uint8_t *base = pieces[order[0]];
     for (int i = 0; i < k; i++) base = std::min(base, pieces[order[i]]);
@@ -811,11 +879,372 @@ int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const
         a.copy_off[i] = ids[i] < k ? (int64_t)ids[i] * ess : -1;
         bits = bits && aligned16(p);
     }
-    std::vector<int64_t> out_off(std::max<size_t>(plan->missing.size(), 1));
-    for (size_t r = 0; r < plan->missing.size(); r++) out_off[r] = (int64_t)plan->missing[r] * ess;
+    std::vector<int64_t> out_off(std::max<size_t>(plan.missing.size(), 1));
+    for (size_t r = 0; r < plan.missing.size(); r++) out_off[r] = (int64_t)plan.missing[r] * ess;
     fill_geometry(a, ess, nstripes, nseg);
     if (!bits) a.cps = 1;
-    return run_matmul(c, a, out_off.data(), *plan, nseg, bits, s);
+    return run_matmul(c, a, out_off.data(), plan, nseg, bits, s);
+}
+
+// Core rebuild: device pointers of the nshares pieces, nstripes stripes of
+// share size `ess`, out stripe-major; batched over nseg with strides.  The
+// plan is made here if the context has none (synchronous: the per-stripe
+// calls, the host pipeline and Decode's correction path, which all wait anyway;
+// the asynchronous batched rebuild goes through rebuild_async).
+int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int ess, int64_t nstripes,
+                   int64_t nseg, int64_t piece_seg_stride, int64_t out_seg_stride, uint8_t *out, hipStream_t s) {
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    PlanPtr plan;
+    rc = get_plan(c, ids, &plan);
+    if (rc) return rc;
+    return rebuild_with_plan(c, *plan, order, ids, pieces, ess, nstripes, nseg, piece_seg_stride, out_seg_stride, out,
+                             s);
+}
+
+// ---------------------------------------------------------------- share-set calls (rs_sets.hpp)
+
+// One segment of a share-set call as the host prepares it: the inputs in the
+// kernel's order (infectious' k chosen shares by position, then -- Decode --
+// the other shares by number) and the rows (missing data positions, then one
+// syndrome row per non-basis input).
+struct SetSeg {
+    const uint8_t *in[kMaxOps];
+    int num[kMaxOps];
+    int missing[kMaxOps];
+    int nin = 0, nstore = 0, rows = 0, nw = 2;
+    uint8_t *out = nullptr;
+};
+
+// Fill `sg` for one segment given as (nshares, nums, pieces).  Errors as
+// Rebuild / Decode report them (NotEnoughShares, invalid share id, a repeated
+// share chosen twice: singular).
+int set_segment(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, uint8_t *out,
+                bool decode, SetSeg &sg) {
+    const int k = c->k;
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    if (decode)
+        for (int i = 0; i < nshares; i++)
+            if (nums[i] < 0 || nums[i] >= c->n) return EC_ERR_INVALID_SHARE;
+    bool seen[256] = {};
+    sg.nin = k;
+    sg.nstore = 0;
+    for (int i = 0; i < k; i++) {
+        if (seen[ids[i]]) return EC_ERR_SINGULAR;
+        seen[ids[i]] = true;
+        sg.in[i] = pieces[order[i]];
+        sg.num[i] = ids[i];
+        if (ids[i] >= k) sg.missing[sg.nstore++] = i;
+    }
+    if (decode) {
+        if (nshares > kMaxOps) return EC_ERR_UNSUPPORTED;
+        std::vector<char> chosen(nshares, 0);
+        for (int i = 0; i < k; i++) chosen[order[i]] = 1;
+        std::vector<int> rest;
+        for (int i = 0; i < nshares; i++)
+            if (!chosen[i]) rest.push_back(i);
+        std::stable_sort(rest.begin(), rest.end(), [&](int x, int y) { return nums[x] < nums[y]; });
+        for (int i : rest) {
+            sg.in[sg.nin] = pieces[i];
+            sg.num[sg.nin++] = nums[i];
+        }
+    }
+    sg.rows = sg.nstore + (sg.nin - k);
+    sg.nw = sets_waves(sg.rows);
+    sg.out = out;
+    return EC_OK;
+}
+
+// The slots' host memory is read by rs_sets_prep and written by the launches'
+// last workgroup straight over the bus: coherent (uncached on the GPU side), so
+// a slot reused by the next call is never read from a stale cache line.
+constexpr unsigned kSetsHostFlags = hipHostMallocCoherent | hipHostMallocMapped;
+
+// A free slot of the ring with room for nseg segments and tgt_words words of
+// leaf tables (waits while kMaxSlots calls are in flight on the GPU).
+SetsSlot *sets_acquire(ec_ctx *c, size_t nseg, size_t tgt_words) {
+    SetsRing &R = c->sets;
+    SetsSlot *sl = nullptr;
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(R.mu);
+            for (auto &x : R.slots)
+                if (x->idle()) {
+                    sl = x.get();
+                    break;
+                }
+            if (!sl && R.slots.size() < SetsRing::kMaxSlots) {
+                auto x = std::make_unique<SetsSlot>();
+                if (hipHostMalloc((void **)&x->h_words, 4 * 65, kSetsHostFlags) != hipSuccess) return nullptr;
+                memset(x->h_words, 0, 4 * 65);
+                x->stage_cap = 0;
+                R.slots.push_back(std::move(x));
+                sl = R.slots.back().get();
+            }
+            if (sl) sl->busy = true;
+        }
+        if (sl) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    // (the slot is ours, and the GPU is done with it: its buffers may be replaced)
+    bool ok = true;
+    if (sl->stage_cap < nseg) {
+        const size_t cap = std::max<size_t>(32, (nseg + 31) & ~(size_t)31);
+        if (sl->h_stage) (void)hipHostFree(sl->h_stage);
+        if (sl->d_desc) (void)hipFree(sl->d_desc);
+        if (sl->d_words) (void)hipFree(sl->d_words);
+        sl->h_stage = nullptr, sl->d_desc = nullptr, sl->d_words = nullptr;
+        ok = hipHostMalloc((void **)&sl->h_stage, cap * sizeof(SetStage), kSetsHostFlags) == hipSuccess &&
+             hipMalloc(&sl->d_desc, cap * sizeof(SetDesc)) == hipSuccess &&
+             hipMalloc(&sl->d_words, 4 * (cap + 1)) == hipSuccess;
+        if (ok && cap + 1 > 65) {
+            uint32_t *hw = nullptr;
+            ok = hipHostMalloc((void **)&hw, 4 * (cap + 1), kSetsHostFlags) == hipSuccess;
+            if (ok) {
+                hw[0] = sl->seq;
+                (void)hipHostFree(sl->h_words);
+                sl->h_words = hw;
+            }
+        }
+        sl->stage_cap = ok ? cap : 0;
+    }
+    if (ok && sl->tgt_cap < tgt_words) {
+        const size_t cap = std::max<size_t>(tgt_words, (size_t)32 * 8192);
+        if (sl->d_tgt) (void)hipFree(sl->d_tgt);
+        sl->d_tgt = nullptr;
+        ok = hipMalloc(&sl->d_tgt, cap * 8) == hipSuccess;
+        sl->tgt_cap = ok ? cap : 0;
+    }
+    if (!ok) {
+        std::lock_guard<std::mutex> g(R.mu);
+        sl->busy = false;
+        return nullptr;
+    }
+    return sl;
+}
+
+void sets_release(ec_ctx *c, SetsSlot *sl) {
+    std::lock_guard<std::mutex> g(c->sets.mu);
+    sl->busy = false;
+}
+
+// The share-set pass over segs (each nstripes stripes): rs_sets_prep, then one
+// rs_matmul_sets launch per wave-count class, all on stream s.  With `bad`
+// (Decode), waits and returns per segment the count of syndrome failures.
+int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_t s, std::vector<uint32_t> *bad) {
+    const int k = c->k, ess = c->ess;
+    const size_t nseg = segs.size();
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    std::vector<int> idx(nseg);
+    for (size_t g = 0; g < nseg; g++) idx[g] = (int)g;
+    std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return segs[x].nw < segs[y].nw; });
+    std::vector<size_t> toff(nseg);
+    size_t words = 0;
+    for (size_t q = 0; q < nseg; q++) {
+        toff[q] = words;
+        words += (sets_tgt_entries(segs[idx[q]].nin, segs[idx[q]].rows) + 7) & ~(size_t)7;
+    }
+    SetsSlot *sl = sets_acquire(c, nseg, words);
+    if (!sl) return EC_ERR_DEVICE;
+    for (size_t q = 0; q < nseg; q++) {
+        const SetSeg &sg = segs[idx[q]];
+        SetStage &st = sl->h_stage[q];
+        SetDesc &d = st.d;
+        for (int j = 0; j < sg.nin; j++) {
+            d.in[j] = sg.in[j];
+            d.copy_off[j] = j < k && sg.num[j] < k ? sg.num[j] * ess : -1;
+            st.num[j] = sg.num[j];
+        }
+        for (int r = 0; r < sg.nstore; r++) {
+            d.out_off[r] = sg.missing[r] * ess;
+            st.missing[r] = sg.missing[r];
+        }
+        d.out = sg.out;
+        d.tgt = sl->d_tgt + toff[q];
+        d.zero_check = bad ? sl->d_words + 1 + q : nullptr;
+        d.nin = sg.nin;
+        d.nout = sg.rows;
+        d.nstore = sg.nstore;
+        d.status = 0;
+        st.k = k;
+        st.nw = sg.nw;
+    }
+    const uint32_t seq = sl->seq + 1;
+    const int64_t chunks = nstripes * (ess / 16), tiles = (chunks + kTileChunksHost - 1) / kTileChunksHost;
+    hipError_t e = launch_sets_prep(sl->h_stage, sl->d_desc, (int)nseg, c->jt_base, sl->d_words, s);
+    if (e != hipSuccess) {  // nothing was queued: the slot is as it was
+        sets_release(c, sl);
+        return hip_fail(e);
+    }
+    for (size_t q0 = 0; q0 < nseg && e == hipSuccess;) {
+        size_t q1 = q0;
+        while (q1 < nseg && segs[idx[q1]].nw == segs[idx[q0]].nw) q1++;
+        SetsArgs a{};
+        a.desc = sl->d_desc + q0;
+        a.nstripes = nstripes;
+        a.chunks_per_seg = chunks;
+        a.tiles_per_seg = tiles;
+        a.total_tiles = tiles * (int64_t)(q1 - q0);
+        a.ess = ess;
+        a.cps = ess / 16;
+        a.k = k;
+        a.done_ctr = sl->d_words;
+        a.host_done = sl->h_words;
+        a.seq = seq;
+        a.total_wgs = (uint32_t)(tiles * (int64_t)nseg);
+        a.chk_flag = c->d_chk;
+        e = launch_matmul_sets(a, segs[idx[q0]].nw, s);
+        q0 = q1;
+    }
+    if (e != hipSuccess) {  // the slot may be half used: never again
+        std::lock_guard<std::mutex> g(c->sets.mu);
+        sl->dead = true;
+        sl->busy = false;
+        return hip_fail(e);
+    }
+    sl->seq = seq;
+    c->last_body = EC_BODY_JUMP_TABLE;
+    int rc = after_launch(c->d_chk, s);
+    if (bad && rc == EC_OK) {
+        // (the slot stays busy until the counts are read: another call may not reuse it before)
+        if (hipMemcpyAsync(sl->h_words + 1, sl->d_words + 1, 4 * nseg, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = EC_ERR_DEVICE;
+        bad->assign(nseg, 0);
+        for (size_t q = 0; q < nseg && rc == EC_OK; q++) (*bad)[idx[q]] = sl->h_words[1 + q];
+    }
+    sets_release(c, sl);
+    return rc;
+}
+
+// ---------------------------------------------------------------- straight-line code in the background
+
+std::mutex g_builders_mu;
+std::set<ec_ctx *> g_builders;  // contexts whose builder thread runs
+
+void sl_worker(ec_ctx *c) {
+    (void)hipSetDevice(c->device);
+    SlBuilder &B = c->slb;
+    for (;;) {
+        std::vector<int> ids;
+        {
+            std::unique_lock<std::mutex> g(B.mu);
+            B.cv.wait(g, [&] { return B.stop || !B.q.empty(); });
+            if (B.stop) break;
+            ids = std::move(B.q.front());
+            B.q.pop_front();
+        }
+        PlanPtr plan;
+        if (get_plan(c, ids, &plan) == EC_OK && plan->rows >= 1 && plan->rows <= kMaxOps) ensure_sl(c, *plan);
+        {
+            std::lock_guard<std::mutex> g(B.mu);
+            B.pending.erase(ids);
+        }
+        B.cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(B.mu);
+    B.pending.clear();
+    B.q.clear();
+    B.cv.notify_all();
+}
+
+// At exit, builders still running finish the plan in hand before the HIP
+// runtime's own exit handlers (registered before this one, on the first HIP
+// call) tear the runtime down under a module load.
+void stop_builders() {
+    std::lock_guard<std::mutex> g(g_builders_mu);
+    for (ec_ctx *c : g_builders) {
+        {
+            std::lock_guard<std::mutex> b(c->slb.mu);
+            c->slb.stop = true;
+        }
+        c->slb.cv.notify_all();
+        if (c->slb.th.joinable()) c->slb.th.join();
+    }
+    g_builders.clear();
+}
+
+void stop_builder(ec_ctx *c) {
+    {
+        std::lock_guard<std::mutex> g(g_builders_mu);
+        g_builders.erase(c);
+        {
+            std::lock_guard<std::mutex> b(c->slb.mu);
+            c->slb.stop = true;
+        }
+        c->slb.cv.notify_all();
+    }
+    if (c->slb.th.joinable()) c->slb.th.join();
+}
+
+// Queue the straight-line code of share set `ids` (no-op if queued already).
+void sl_request(ec_ctx *c, const std::vector<int> &ids) {
+    SlBuilder &B = c->slb;
+    std::lock_guard<std::mutex> g(B.mu);
+    if (B.stop || B.pending.count(ids)) return;
+    if (!B.th.joinable()) {
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(stop_builders); });
+        std::lock_guard<std::mutex> r(g_builders_mu);
+        B.th = std::thread(sl_worker, c);
+        g_builders.insert(c);
+    }
+    B.pending.insert(ids);
+    B.q.push_back(ids);
+    B.cv.notify_all();
+}
+
+// The context's plan for share set ids, if it has one (no plan is made).
+PlanPtr find_plan(ec_ctx *c, const std::vector<int> &ids) {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (auto it = c->plans.begin(); it != c->plans.end(); ++it)
+        if ((*it)->key == ids) {
+            c->plans.splice(c->plans.begin(), c->plans, it);
+            return c->plans.front();
+        }
+    return nullptr;
+}
+
+// The batched rebuild as ec_rebuild_segments_batched runs it: nothing on the
+// launch path waits for the host or another stream.  A share set whose
+// straight-line code is ready runs it; any other runs the share-set pass (its
+// decode rows solved on the GPU, stream-ordered) and, for launches large
+// enough to use it, has its code made in the background.
+int rebuild_async(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int64_t nstripes,
+                  int64_t nseg, int64_t pss, int64_t oss, uint8_t *out, hipStream_t s) {
+    const int k = c->k, ess = c->ess;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    bool bits = ess % 16 == 0 && aligned16(out) && pss % 16 == 0 && oss % 16 == 0;
+    int m = 0;
+    for (int i = 0; i < k; i++) {
+        bits = bits && aligned16(pieces[order[i]]);
+        m += ids[i] >= k;
+    }
+    // byte kernel, forced straight-line code, or nothing to compute (the copy
+    // kernel; its plan has no tables to wait for): the plan path
+    if (!bits || m == 0 || c->body == EC_BODY_STRAIGHT_LINE)
+        return rebuild_device(c, nshares, nums, pieces, ess, nstripes, nseg, pss, oss, out, s);
+    const int64_t tiles = (nstripes * (ess / 16) + kTileChunksHost - 1) / kTileChunksHost * nseg;
+    if (c->body == EC_BODY_AUTO && tiles >= kSlMinTiles) {
+        if (PlanPtr plan = find_plan(c, ids); plan && plan->sl_ready.load(std::memory_order_acquire))
+            return rebuild_with_plan(c, *plan, order, ids, pieces, ess, nstripes, nseg, pss, oss, out, s);
+        sl_request(c, ids);
+    }
+    std::vector<SetSeg> segs(nseg);
+    std::vector<const uint8_t *> pg(nshares);
+    for (int64_t g = 0; g < nseg; g++) {
+        for (int i = 0; i < nshares; i++) pg[i] = pieces[i] + g * pss;
+        rc = set_segment(c, nshares, nums, pg.data(), out + g * oss, false, segs[g]);
+        if (rc) return rc;
+    }
+    return sets_call(c, segs, nstripes, s, nullptr);
 }
 
 }  // namespace
@@ -866,6 +1295,8 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
         for (int j = 0; j < k; j++) c->G[(size_t)i * k + j] = gen_entry(k, i, j);
     c->enc_row.resize(n);
     HIP_TRY(hipStreamCreateWithFlags(&c->setup, hipStreamNonBlocking));
+    // for the share-set pass (rs_sets_prep): where the jump table's leaves are
+    HIP_TRY(jt_table_base_addr(&c->jt_base, c->setup));
     // Scratch of ec_hash_segments / ec_blake3_pieces comes from the default pool
     // in stream order: keep the pool's memory mapped between calls instead of
     // returning it to the driver at every synchronisation.
@@ -889,20 +1320,21 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
 void ec_destroy(ec_ctx *c) {
     if (!c) return;
     DeviceGuard dg(c->device);
+    stop_builder(c);  // (before anything its plan in hand uses goes)
+    // share-set slots still read by launches in flight: wait for the device once
+    {
+        bool busy = false;
+        std::lock_guard<std::mutex> g(c->sets.mu);
+        for (auto &x : c->sets.slots) busy = busy || (!x->dead && __atomic_load_n(x->h_words, __ATOMIC_ACQUIRE) != x->seq);
+        if (busy) (void)hipDeviceSynchronize();
+        c->sets.slots.clear();
+    }
     for (int s = 0; s < HostPipe::kSlots; s++) {
         if (c->pipe.st[s]) (void)hipStreamSynchronize(c->pipe.st[s]), (void)hipStreamDestroy(c->pipe.st[s]);
         if (c->pipe.d_in[s]) (void)hipFree(c->pipe.d_in[s]);
         if (c->pipe.d_out[s]) (void)hipFree(c->pipe.d_out[s]);
     }
-    for (auto &u : c->upload_free) {
-        for (auto st : u->st)
-            if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
-        for (auto e : u->ev)
-            if (e) (void)hipEventDestroy(e);
-        if (u->d_in) (void)hipFree(u->d_in);
-        if (u->d_out) (void)hipFree(u->d_out);
-    }
-    c->upload_free.clear();
+    c->upload_free.clear();  // (UploadSlot's destructor waits for and frees each)
     for (auto &w : c->all_ws) {
         if (w->stream) (void)hipStreamSynchronize(w->stream), (void)hipStreamDestroy(w->stream);
         if (w->d_buf) (void)hipFree(w->d_buf);
@@ -1056,8 +1488,100 @@ int ec_rebuild_segments_batched(const ec_ctx *cc, int nshares, const int *nums, 
     if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
     if (nstripes == 0 || nseg == 0) return EC_OK;
     DeviceGuard dg(c->device);
-    return rebuild_device(c, nshares, nums, pieces, c->ess, (int64_t)nstripes, (int64_t)nseg, piece_seg_stride,
-                          out_seg_stride, out, (hipStream_t)stream);
+    return rebuild_async(c, nshares, nums, pieces, (int64_t)nstripes, (int64_t)nseg, piece_seg_stride, out_seg_stride,
+                         out, (hipStream_t)stream);
+}
+
+// Segment g's shares are entries [off_g, off_g + nshares[g]) of nums / pieces.
+static int sets_export(ec_ctx *c, size_t nseg, const int *nshares, const int *nums, const uint8_t *const *pieces,
+                       size_t nstripes, uint8_t *const *outs, hipStream_t s, bool decode) {
+    const int ess = c->ess;
+    if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    // a call of many segments goes in passes of at most kPass (bounded staging per slot)
+    constexpr size_t kPass = 64;
+    std::vector<SetSeg> segs;
+    std::vector<size_t> seg_of;  // segs[i] is segment seg_of[i] of the call
+    std::vector<size_t> off(nseg + 1, 0);
+    for (size_t g = 0; g < nseg; g++) off[g + 1] = off[g] + (size_t)std::max(nshares[g], 0);
+    auto flush = [&]() -> int {
+        std::vector<uint32_t> bad;
+        int rc = sets_call(c, segs, (int64_t)nstripes, s, decode ? &bad : nullptr);
+        // Decode: a segment whose syndromes are not all zero is corrected (in the
+        // caller's pieces, as infectious corrects share.Data) and rebuilt on its own
+        for (size_t i = 0; i < segs.size() && rc == EC_OK && decode; i++)
+            if (bad[i]) {
+                const size_t g = seg_of[i];
+                rc = ec_decode_segments(c, nshares[g], nums + off[g], (uint8_t *const *)pieces + off[g], nstripes,
+                                        outs[g], (ec_stream)s);
+            }
+        segs.clear();
+        seg_of.clear();
+        return rc;
+    };
+    for (size_t g = 0; g < nseg; g++) {
+        const int ns = nshares[g];
+        if (ns < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+        bool bits = ess % 16 == 0 && aligned16(outs[g]) && (!decode || ns <= kMaxOps);
+        for (int i = 0; i < ns; i++) bits = bits && aligned16(pieces[off[g] + i]);
+        if (!bits) {  // byte kernel / more inputs than a launch takes: this segment on its own
+            const int rc = decode ? ec_decode_segments(c, ns, nums + off[g], (uint8_t *const *)pieces + off[g], nstripes,
+                                                       outs[g], (ec_stream)s)
+                                  : rebuild_device(c, ns, nums + off[g], pieces + off[g], ess, (int64_t)nstripes, 1,
+                                                   0, 0, outs[g], s);
+            if (rc) return rc;
+            continue;
+        }
+        segs.emplace_back();
+        seg_of.push_back(g);
+        if (int rc = set_segment(c, ns, nums + off[g], pieces + off[g], outs[g], decode, segs.back())) return rc;
+        if (segs.size() == kPass)
+            if (int rc = flush()) return rc;
+    }
+    return segs.empty() ? EC_OK : flush();
+}
+
+int ec_rebuild_segments_sets(const ec_ctx *cc, size_t nseg, const int *nshares, const int *nums,
+                             const uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nseg && (!nshares || !nums || !pieces || !outs))) return EC_ERR_INVALID_ARG;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    for (size_t g = 0; g < nseg; g++)
+        if (!outs[g]) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    return sets_export(c, nseg, nshares, nums, pieces, nstripes, outs, (hipStream_t)stream, false);
+}
+
+int ec_decode_segments_sets(const ec_ctx *cc, size_t nseg, const int *nshares, const int *nums,
+                            uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nseg && (!nshares || !nums || !pieces || !outs))) return EC_ERR_INVALID_ARG;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    for (size_t g = 0; g < nseg; g++)
+        if (!outs[g]) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    int rc = sets_export(c, nseg, nshares, nums, (const uint8_t *const *)pieces, nstripes, outs, (hipStream_t)stream,
+                         true);
+    if (rc == EC_OK && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = EC_ERR_DEVICE;
+    return rc;
+}
+
+int ec_prepare_rebuild(const ec_ctx *cc, int nshares, const int *nums, int wait) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !nums) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    std::vector<int> order, ids;
+    if (int rc = choose_shares(c, nshares, nums, order, ids)) return rc;
+    int m = 0;
+    for (int i = 0; i < c->k; i++) m += ids[i] >= c->k;
+    if (m == 0 || c->k > kMaxOps || c->ess % 16) return 0;  // (no code to make: copies, or the byte kernel)
+    if (PlanPtr p = find_plan(c, ids); p && p->sl_ready.load(std::memory_order_acquire)) return 1;
+    sl_request(c, ids);
+    if (wait) {
+        std::unique_lock<std::mutex> g(c->slb.mu);
+        c->slb.cv.wait(g, [&] { return c->slb.pending.count(ids) == 0; });
+    }
+    PlanPtr p = find_plan(c, ids);
+    return p && p->sl_ready.load(std::memory_order_acquire) ? 1 : 0;
 }
 
 int ec_rebuild_segments(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces,
@@ -1500,6 +2024,14 @@ struct ec_upload {
     std::vector<size_t> end;  // end stripe of each chunk
     std::atomic<int> rc{EC_OK};
     std::atomic<int> done{0};  // leading chunks known to be in host memory
+    int n = 0;                 // pieces hashed (EC_FLAG_HASH_PIECES), 0 without
+    // ec_upload_end waits for the callers inside ec_upload_wait / _ready /
+    // _hashes before it frees the handle (piece readers block in
+    // those while another thread closes the segment)
+    std::mutex mu;
+    std::condition_variable cv;
+    int inside = 0;
+    bool ending = false;
 };
 
 static void upload_release(ec_upload *u) {
@@ -1510,12 +2042,46 @@ static void upload_release(ec_upload *u) {
     u->c->upload_free.push_back(std::move(u->slot));
 }
 
+// A caller inside one of the waiting calls on u (released by the destructor).
+struct UploadUse {
+    ec_upload *u;
+    bool ok;
+    explicit UploadUse(ec_upload *x) : u(x) {
+        std::lock_guard<std::mutex> g(u->mu);
+        ok = !u->ending;
+        if (ok) u->inside++;
+    }
+    ~UploadUse() {
+        if (!ok) return;
+        std::lock_guard<std::mutex> g(u->mu);
+        if (--u->inside == 0) u->cv.notify_all();
+    }
+};
+
+// The piece hashes of a streamed upload, chunk by chunk: after the encode of
+// each chunk of stripes, the chaining values of the BLAKE3 chunks that chunk
+// completes in every piece (data pieces straight from the segment, parity from
+// the encoder's output), on a stream of their own; after the last, the tree
+// fold and the hashes' copy to pinned memory.  The reference hashes each piece
+// as it streams through a TeeReader and needs the sum only at the end
+// (piecestore/upload.go:155,262-270): so does this.  A chunk boundary that
+// does not fall on a 1-KiB boundary of the pieces (a caller's chunk size), or
+// pieces of one BLAKE3 chunk, hash everything after the last chunk instead.
+static bool upload_hash_streamed(const ec_ctx *c, const std::vector<size_t> &end, size_t nstripes) {
+    const uint64_t plen = (uint64_t)nstripes * c->ess;
+    if (plen < 2048) return false;
+    for (size_t i = 0; i + 1 < end.size(); i++)
+        if ((end[i] * (uint64_t)c->ess) % 1024) return false;
+    return true;
+}
+
 int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8_t *pieces, int flags,
                     size_t chunk_stripes, ec_upload **out) {
     ec_ctx *c = const_cast<ec_ctx *>(cc);
     if (!out) return EC_ERR_INVALID_ARG;
     *out = nullptr;
     if (!c || !seg || !pieces) return EC_ERR_INVALID_ARG;
+    if (flags & ~(EC_FLAG_PARITY_ONLY | EC_FLAG_HASH_PIECES)) return EC_ERR_INVALID_ARG;
     DeviceGuard dg(c->device);
     std::unique_ptr<ec_upload> u(new ec_upload());
     u->c = c;
@@ -1528,8 +2094,16 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
     const size_t nch = u->end.size();
     const size_t ess = c->ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
     const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
+    const bool hashed = (flags & EC_FLAG_HASH_PIECES) != 0;
     const int rows = parity_only ? c->n - c->k : c->n;
     const size_t plen = nstripes * ess, pbytes = (size_t)rows * plen;
+    const bool streamed_hash = hashed && upload_hash_streamed(c, u->end, nstripes);
+    const uint64_t nb3 = (plen + 1023) / 1024;  // BLAKE3 chunks per piece
+    // hash area: [n][nb3][8] chunk CVs | n*32 hashes | scratch (fold, or the one-pass hash's)
+    const size_t cvs_bytes = streamed_hash ? align_up((size_t)c->n * nb3 * 32, 256) : 0;
+    const size_t hash_bytes = align_up(32 * (size_t)c->n, 256);
+    const size_t scratch = streamed_hash ? b3_fold_ws_bytes(c->n, nb3) : b3_segment_ws_bytes(c, 1, nstripes);
+    const size_t hcap = hashed ? cvs_bytes + hash_bytes + std::max<size_t>(scratch, 256) : 0;
     {
         std::lock_guard<std::mutex> g(c->upload_mu);
         if (!c->upload_free.empty()) {
@@ -1555,12 +2129,32 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
         HIP_TRY(hipMalloc(&sl.d_out, std::max<size_t>(pbytes, 1)));
         sl.out_cap = pbytes;
     }
-    while (sl.ev.size() < 3 * nch) {
+    if (hashed && sl.hash_cap < hcap) {
+        if (sl.d_hash) (void)hipFree(sl.d_hash);
+        sl.d_hash = nullptr;
+        sl.hash_cap = 0;
+        HIP_TRY(hipMalloc(&sl.d_hash, hcap));
+        sl.hash_cap = hcap;
+    }
+    if (hashed && sl.h_hash_cap < 32 * (size_t)c->n) {
+        if (sl.h_hash) (void)hipHostFree(sl.h_hash);
+        sl.h_hash = nullptr;
+        sl.h_hash_cap = 0;
+        HIP_TRY(hipHostMalloc((void **)&sl.h_hash, 32 * (size_t)c->n, hipHostMallocDefault));
+        sl.h_hash_cap = 32 * (size_t)c->n;
+    }
+    while (sl.ev.size() < 3 * nch + 1) {
         hipEvent_t e = nullptr;
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         sl.ev.push_back(e);
     }
-    hipStream_t h2d = sl.st[0], comp = sl.st[1], d2h = sl.st[2];
+    hipStream_t h2d = sl.st[0], comp = sl.st[1], d2h = sl.st[2], hs = sl.st[3];
+    uint32_t *cvs = (uint32_t *)sl.d_hash;
+    uint8_t *d_hashes = sl.d_hash + cvs_bytes, *d_scratch = d_hashes + hash_bytes;
+    const uint8_t *d_parity = sl.d_out + (parity_only ? 0 : (size_t)c->k * plen);
+    B3View pv = parity_view(c, d_parity, 1, nstripes);
+    if (c->n == c->k) pv.npieces = 0;
+    const B3View dv = data_view(c, sl.d_in, 1, nstripes);
     int rc = EC_OK;
     for (size_t ch = 0; ch < nch && rc == EC_OK; ch++) {
         const size_t s0 = ch ? u->end[ch - 1] : 0, s1 = u->end[ch];
@@ -1571,13 +2165,31 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
             rc = EC_ERR_DEVICE;
             break;
         }
-        if (rows > 0) rc = encode_range(c, sl.d_in, 1, nstripes, s0, s1, sl.d_out, flags, comp);
+        if (rows > 0) rc = encode_range(c, sl.d_in, 1, nstripes, s0, s1, sl.d_out, flags & EC_FLAG_PARITY_ONLY, comp);
         if (rc) break;
         if (hipEventRecord(e_enc, comp) != hipSuccess || hipStreamWaitEvent(d2h, e_enc, 0) != hipSuccess ||
             (rows > 0 && hipMemcpy2DAsync(pieces + s0 * ess, plen, sl.d_out + s0 * ess, plen, (s1 - s0) * ess, rows,
                                           hipMemcpyDeviceToHost, d2h) != hipSuccess) ||
             hipEventRecord(e_out, d2h) != hipSuccess)
             rc = EC_ERR_DEVICE;
+        // this chunk's BLAKE3 chunks of every piece, off the encode's critical path
+        if (rc == EC_OK && streamed_hash) {
+            const uint64_t c0 = s0 * ess / 1024, c1 = ch + 1 == nch ? nb3 : s1 * ess / 1024;
+            if (hipStreamWaitEvent(hs, e_enc, 0) != hipSuccess ||
+                b3_launch_chunk_range(dv, pv, c0, c1, cvs, hs) != hipSuccess)
+                rc = EC_ERR_DEVICE;
+        }
+    }
+    if (rc == EC_OK && hashed) {
+        hipError_t e = hipStreamWaitEvent(hs, sl.ev[2 * nch - 1], 0);  // (the last encode)
+        if (e == hipSuccess)
+            e = streamed_hash ? b3_launch_fold(cvs, c->n, nb3, d_hashes, d_scratch, hs)
+                              : (hash_segments(c, sl.d_in, d_parity, 1, nstripes, d_hashes, d_scratch, hs) == EC_OK
+                                     ? hipSuccess : hipErrorUnknown);
+        if (e == hipSuccess) e = hipMemcpyAsync(sl.h_hash, d_hashes, 32 * (size_t)c->n, hipMemcpyDeviceToHost, hs);
+        if (e == hipSuccess) e = hipEventRecord(sl.ev[3 * nch], hs);
+        if (e != hipSuccess) rc = hip_fail(e);
+        u->n = c->n;
     }
     u->rc.store(rc);
     if (rc) {
@@ -1588,11 +2200,7 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
     return EC_OK;
 }
 
-// Any number of threads may wait on one upload (one per piece reader); the
-// event waits run without a lock, and the count of done chunks only grows.
-int ec_upload_wait(ec_upload *u, size_t stripes) {
-    if (!u) return EC_ERR_INVALID_ARG;
-    DeviceGuard dg(u->c->device);
+static int upload_wait_chunks(ec_upload *u, size_t stripes) {
     const int nch = (int)u->end.size();
     for (;;) {
         if (const int rc = u->rc.load()) return rc;
@@ -1606,8 +2214,20 @@ int ec_upload_wait(ec_upload *u, size_t stripes) {
     }
 }
 
+// Any number of threads may wait on one upload (one per piece reader); the
+// event waits run without a lock, and the count of done chunks only grows.
+int ec_upload_wait(ec_upload *u, size_t stripes) {
+    if (!u) return EC_ERR_INVALID_ARG;
+    UploadUse use(u);
+    if (!use.ok) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(u->c->device);
+    return upload_wait_chunks(u, stripes);
+}
+
 size_t ec_upload_ready(ec_upload *u) {
     if (!u || u->rc.load()) return 0;
+    UploadUse use(u);
+    if (!use.ok) return 0;
     DeviceGuard dg(u->c->device);
     const int nch = (int)u->end.size();
     for (int d = u->done.load(); d < nch && hipEventQuery(u->slot->ev[2 * nch + d]) == hipSuccess; d = u->done.load())
@@ -1616,12 +2236,27 @@ size_t ec_upload_ready(ec_upload *u) {
     return d ? u->end[d - 1] : 0;
 }
 
+int ec_upload_hashes(ec_upload *u, uint8_t *hashes) {
+    if (!u || !hashes) return EC_ERR_INVALID_ARG;
+    UploadUse use(u);
+    if (!use.ok || u->n == 0) return EC_ERR_INVALID_ARG;  // (begun without EC_FLAG_HASH_PIECES)
+    if (const int rc = u->rc.load()) return rc;
+    DeviceGuard dg(u->c->device);
+    if (hipEventSynchronize(u->slot->ev[3 * u->end.size()]) != hipSuccess) return EC_ERR_DEVICE;
+    memcpy(hashes, u->slot->h_hash, 32 * (size_t)u->n);
+    return EC_OK;
+}
+
 int ec_upload_end(ec_upload *u) {
     if (!u) return EC_ERR_INVALID_ARG;
     int rc = u->rc.load();
     {
         DeviceGuard dg(u->c->device);
-        if (rc == EC_OK) rc = ec_upload_wait(u, SIZE_MAX);
+        if (rc == EC_OK) rc = upload_wait_chunks(u, SIZE_MAX);
+        std::unique_lock<std::mutex> g(u->mu);
+        u->ending = true;  // new callers are turned away; those inside finish first
+        u->cv.wait(g, [&] { return u->inside == 0; });
+        g.unlock();
         upload_release(u);
     }
     delete u;
@@ -1933,7 +2568,7 @@ int ec_decode(const ec_ctx *cc, int nshares, int *nums, uint8_t **shares, size_t
     if (!out) return EC_ERR_INVALID_ARG;
     for (int i = 0; i < nshares; i++)
         if (nums[i] < 0 || nums[i] >= c->n) return EC_ERR_INVALID_SHARE;
-    if (k > kMaxOps || nshares - k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
     const CorrectLayout L(share_len, nshares, k, share_len * k);
     Workspace *w = acquire_ws(c, L.bytes);
     if (!w->d_buf || !w->stream) { release_ws(c, w); return EC_ERR_DEVICE; }
@@ -2053,20 +2688,25 @@ int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in
     std::vector<int> ord(nshares);
     for (int i = 0; i < nshares; i++) ord[i] = i;
     std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return nums_in[x] < nums_in[y]; });
-    // a launch takes at most kMaxOps inputs: of more shares (a wide code, n > 128), the first
-    // kMaxOps in number order are checked, corrected and rebuilt from (every data share present
-    // among them; the rest are neither read nor corrected)
-    nshares = std::min(nshares, kMaxOps);
-    std::vector<int> nums(nshares);
-    std::vector<uint8_t *> pcs(nshares);
-    for (int i = 0; i < nshares; i++) {
-        nums[i] = nums_in[ord[i]];
-        pcs[i] = pieces_in[ord[i]];
+    // a launch takes at most kMaxOps inputs.  Of more shares (a wide code, n > 128) the first
+    // kMaxOps in number order go through the one-pass check + rebuild, and the syndromes of the
+    // others are checked in further launches of kMaxOps - k of them at a time against the same
+    // basis (the first k); a segment with errors is corrected over all of them, as infectious'
+    // Correct uses every share it is given (rs.go:32-38)
+    const int ns_all = nshares;
+    std::vector<int> nums_all(ns_all);
+    std::vector<uint8_t *> pcs_all(ns_all);
+    for (int i = 0; i < ns_all; i++) {
+        nums_all[i] = nums_in[ord[i]];
+        pcs_all[i] = pieces_in[ord[i]];
     }
+    nshares = std::min(nshares, kMaxOps);
+    std::vector<int> nums(nums_all.begin(), nums_all.begin() + nshares);
+    std::vector<uint8_t *> pcs(pcs_all.begin(), pcs_all.begin() + nshares);
     const int extra = nshares - k;
     const size_t piece_len = nstripes * (size_t)ess;
     bool bits = ess % 16 == 0 && aligned16(out);
-    for (auto p : pcs) bits = bits && aligned16(p);
+    for (auto p : pcs_all) bits = bits && aligned16(p);
     Workspace *w = nullptr;
     int rc = EC_OK;
     uint32_t nbad = bits ? 0u : 1u;  // no bit-sliced check: take the workspace path
@@ -2136,37 +2776,74 @@ int ec_decode_segments_batched(const ec_ctx *cc, int nshares, const int *nums_in
     if (!rc && !fused)
         rc = rebuild_device(c, nshares, nums.data(), cp.data(), ess, (int64_t)nstripes, (int64_t)nseg,
                             piece_seg_stride, out_seg_stride, out, s);
+    // the shares past the first kMaxOps: their syndromes, a block of kMaxOps - k at a time
+    if (ns_all > nshares && k >= kMaxOps) nbad = 1;  // (no room for a syndrome row in a launch: Correct checks)
+    for (int lo = nshares; !rc && bits && k < kMaxOps && lo < ns_all; lo += kMaxOps - k) {
+        const int hi = std::min(ns_all, lo + (kMaxOps - k));
+        if (!w) {
+            w = acquire_ws(c, 16);
+            if (!w->d_buf) { release_ws(c, w); return EC_ERR_DEVICE; }
+            if (hipMemsetAsync(w->d_buf, 0, 4, s) != hipSuccess) rc = EC_ERR_DEVICE;
+        }
+        std::vector<int> sub(nums_all.begin(), nums_all.begin() + k);
+        std::vector<uint8_t *> sp(pcs_all.begin(), pcs_all.begin() + k);
+        sub.insert(sub.end(), nums_all.begin() + lo, nums_all.begin() + hi);
+        sp.insert(sp.end(), pcs_all.begin() + lo, pcs_all.begin() + hi);
+        PlanPtr plan;
+        if (!rc) rc = syndrome_plan(c, sub, &plan);
+        if (rc) break;
+        RsArgs a{};
+        const uint8_t *base = sp[0];
+        for (auto p : sp) base = std::min<const uint8_t *>(base, p);
+        a.in_base = base;
+        a.in_stripe_stride = ess;
+        a.out_stripe_stride = ess;
+        for (size_t i = 0; i < sp.size(); i++) {
+            a.in_off[i] = sp[i] - base;
+            a.copy_off[i] = -1;
+        }
+        a.in_seg_stride = piece_seg_stride;
+        a.zero_check = (uint32_t *)w->d_buf;
+        std::vector<int64_t> out_off(std::max(hi - lo, 1), 0);
+        fill_geometry(a, ess, (int64_t)nstripes, (int64_t)nseg);
+        rc = run_matmul(c, a, out_off.data(), *plan, (int64_t)nseg, true, s);
+        if (!rc && hipMemcpyAsync(&nbad, w->d_buf, 4, hipMemcpyDeviceToHost, s) != hipSuccess) rc = EC_ERR_DEVICE;
+    }
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EC_ERR_DEVICE;  // returns when done (header)
     if (w) {  // (released before the error path takes a workspace of its own)
         if (rc) (void)hipStreamSynchronize(s);
         release_ws(c, w);
     }
-    if (extra > 0 && !rc) {
+    if (ns_all > k && !rc) {
+        std::vector<const uint8_t *> cpa(ns_all);
         for (size_t g = 0; g < nseg && nbad != 0 && !rc; g++) {
-            // errors (or no bit-sliced check): segment by segment, Correct in a
-            // workspace, write the corrected shares back into the caller's pieces
-            // (infectious corrects share.Data in place), Rebuild again from them
-            for (int i = 0; i < nshares; i++) {
-                pcs[i] = pieces_in[ord[i]] + (int64_t)g * piece_seg_stride;
-                cp[i] = pcs[i];
+            // errors (or no bit-sliced check): segment by segment, Correct over every share in
+            // a workspace, write the corrected shares back into the caller's pieces (infectious
+            // corrects share.Data in place), Rebuild again from them
+            for (int i = 0; i < ns_all; i++) {
+                pcs_all[i] = pieces_in[ord[i]] + (int64_t)g * piece_seg_stride;
+                cpa[i] = pcs_all[i];
             }
             uint8_t *gout = out + (int64_t)g * out_seg_stride;
-            const CorrectLayout L(piece_len, nshares, k, 0);
+            const CorrectLayout L(piece_len, ns_all, k, 0);
             Workspace *cw = acquire_ws(c, L.bytes);
             if (!cw->d_buf || !cw->stream) rc = EC_ERR_DEVICE;
             hipStream_t st = cw->stream;
-            for (int i = 0; i < nshares && !rc; i++)
-                if (hipMemcpyAsync(cw->d_buf + L.slot * i, pcs[i], piece_len, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            for (int i = 0; i < ns_all && !rc; i++)
+                if (hipMemcpyAsync(cw->d_buf + L.slot * i, pcs_all[i], piece_len, hipMemcpyDeviceToDevice, st) !=
+                    hipSuccess)
                     rc = EC_ERR_DEVICE;
             bool changed = false;
-            if (!rc) rc = correct_device(c, cw->d_buf, L, piece_len, nums.data(), nshares, st, &changed);
-            for (int i = 0; i < nshares && !rc && changed; i++)
-                if (hipMemcpyAsync(pcs[i], cw->d_buf + L.slot * i, piece_len, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            if (!rc) rc = correct_device(c, cw->d_buf, L, piece_len, nums_all.data(), ns_all, st, &changed);
+            for (int i = 0; i < ns_all && !rc && changed; i++)
+                if (hipMemcpyAsync(pcs_all[i], cw->d_buf + L.slot * i, piece_len, hipMemcpyDeviceToDevice, st) !=
+                    hipSuccess)
                     rc = EC_ERR_DEVICE;
             if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = EC_ERR_DEVICE;
             if (cw->stream) (void)hipStreamSynchronize(st);
             release_ws(c, cw);
-            if (!rc && changed) rc = rebuild_device(c, nshares, nums.data(), cp.data(), ess, (int64_t)nstripes, 1, 0, 0, gout, s);
+            if (!rc && changed)
+                rc = rebuild_device(c, ns_all, nums_all.data(), cpa.data(), ess, (int64_t)nstripes, 1, 0, 0, gout, s);
             if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = EC_ERR_DEVICE;
         }
     }

@@ -45,8 +45,6 @@ __global__ void rs_flag_columns(const uint8_t *shares, int64_t stride, const uin
     }
 }
 
-constexpr int kMaxDim = 128;
-
 // rows[0..nrows) of shares against expected rows 0..nrows-1: flag the columns that differ
 __global__ void rs_flag_rows(const uint8_t *shares, int64_t stride, const int *rows, int nrows,
                              const uint8_t *expected, int64_t estride, int64_t len, uint8_t *flags) {
@@ -69,6 +67,10 @@ __global__ void rs_put_rows(uint8_t *shares, int64_t stride, const int *rows, in
     }
 }
 
+// kMaxDim: the largest system the instantiation solves (k + 2e <= shares given):
+// 128, and 256 for wide codes given more than 128 shares (n up to 256; its LDS
+// -- 66 KB -- leaves a CU two such workgroups, so it is launched only for those)
+template <int kMaxDim>
 __global__ __launch_bounds__(64) void rs_berlekamp_welch(uint8_t *shares, int64_t stride, int64_t len,
                                                          const int *nums, int k, int n, int ns, const int64_t *cols,
                                                          int ncols, int *status, uint8_t *changed) {
@@ -198,8 +200,13 @@ hipError_t launch_berlekamp_welch(uint8_t *shares, int64_t stride, int64_t len, 
                                   const int64_t *cols, int ncols, int *status, hipStream_t s, uint8_t *changed) {
     int blocks = ncols < 2048 ? ncols : 2048;
     if (blocks < 1) return hipSuccess;
-    hipLaunchKernelGGL(rs_berlekamp_welch, dim3(blocks), dim3(64), 0, s, shares, stride, len, nums, k, n, ns, cols,
-                       ncols, status, changed);
+    const int e = (ns - k) / 2;
+    if (k + 2 * e <= 128)
+        hipLaunchKernelGGL(rs_berlekamp_welch<128>, dim3(blocks), dim3(64), 0, s, shares, stride, len, nums, k, n, ns,
+                           cols, ncols, status, changed);
+    else
+        hipLaunchKernelGGL(rs_berlekamp_welch<256>, dim3(blocks), dim3(64), 0, s, shares, stride, len, nums, k, n, ns,
+                           cols, ncols, status, changed);
     return hipGetLastError();
 }
 

@@ -43,6 +43,7 @@
 #include "gf256_field.hpp"
 #include "rs_device.hpp"
 #include "rs_kernels.hpp"
+#include "rs_sets.hpp"
 #include "rs_sl.hpp"
 
 namespace uplink_ec {
@@ -356,6 +357,10 @@ int jt_waves(int nout) { return nout <= 2 * kJtRows ? 2 : nout <= 3 * kJtRows ? 
 // aligned in 8 slots (jt_inputs enters at call site 8 - count).
 __global__ __launch_bounds__(256) void rs_jt_targets(const RsArgs a, int nw, uint64_t *tgt) {
     const uint64_t base = jt_table_base();
+    if (nw == 0) {  // jt_table_base_addr: only the address of leaf 0
+        if (threadIdx.x == 0) tgt[0] = base;
+        return;
+    }
     constexpr int OPW = kJtRows;
     const int npass = a.nout > 0 ? (a.nout + nw * OPW - 1) / (nw * OPW) : 1;
     const int per_pass = a.nin * nw * OPW;
@@ -457,6 +462,19 @@ size_t jt_targets_bytes(const RsArgs &a) {
 hipError_t launch_jt_targets(const RsArgs &a, uint64_t *targets, hipStream_t s) {
     hipLaunchKernelGGL(rs_jt_targets, dim3(1), dim3(256), 0, s, a, jt_waves(a.nout), targets);
     return hipGetLastError();
+}
+
+hipError_t jt_table_base_addr(uint64_t *out, hipStream_t s) {
+    uint64_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(uint64_t));
+    if (e != hipSuccess) return e;
+    RsArgs a{};
+    hipLaunchKernelGGL(rs_jt_targets, dim3(1), dim3(64), 0, s, a, 0, d);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    return e;
 }
 
 namespace {

@@ -133,15 +133,42 @@ class PinnedBackend:
         return self._mem if (not self._closed and self._mem.nbytes >= total) else None
 
 
-class _PieceStream:
+class _OwnedStream:
+    """A piece stream keeps its SegmentPieceReader alive and counted: the
+    reader's pinned buffers (the padded segment the data pieces are views of,
+    the parity the engine writes) go back to the pool only once the reader is
+    closed and every stream it handed out is closed or gone (a view
+    into a pooled buffer read after another segment took it would send that
+    segment's bytes)."""
+
+    def __init__(self, owner):
+        self._owner = owner
+
+    def close(self):
+        owner, self._owner = self._owner, None
+        if owner is not None:
+            owner._stream_closed()
+        return None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _PieceStream(_OwnedStream):
     """io.ReadCloser over one piece.  `ready(end)` is called before bytes
     [.., end) are read: for a parity piece of a streamed upload it blocks
     until the stripes holding them are in host memory (ec_upload_wait)."""
 
-    def __init__(self, src: np.ndarray, ready=None):
+    def __init__(self, src: np.ndarray, ready=None, owner=None):
+        super().__init__(owner)
         self._src, self._off, self._ready = src, 0, ready
 
     def read(self, n: int = -1) -> bytes:
+        if self._src is None:
+            raise EEStreamError("read from closed piece reader")
         end = self._src.size if n is None or n < 0 else min(self._src.size, self._off + n)
         if self._ready is not None and end > self._off:
             self._ready(end)
@@ -150,19 +177,23 @@ class _PieceStream:
         return b
 
     def close(self):
-        return None
+        self._src = None
+        return super().close()
 
 
-class _DataPieceStream:
+class _DataPieceStream(_OwnedStream):
     """A data piece (num < k) is share num of every stripe of the padded
     segment (EncodeSingle copies it, rs.go:21-23): gathered per read from the
     host segment, with no engine call and nothing to wait for."""
 
-    def __init__(self, padded: np.ndarray, num: int):
+    def __init__(self, padded: np.ndarray, num: int, owner=None):
+        super().__init__(owner)
         self._p, self._num, self._off = padded, num, 0  # padded: [stripes][k][ess]
         self._size = padded.shape[0] * padded.shape[2]
 
     def read(self, n: int = -1) -> bytes:
+        if self._p is None:
+            raise EEStreamError("read from closed piece reader")
         end = self._size if n is None or n < 0 else min(self._size, self._off + n)
         if end <= self._off:
             return b""
@@ -173,7 +204,8 @@ class _DataPieceStream:
         return b
 
     def close(self):
-        return None
+        self._p = None
+        return super().close()
 
 
 class SegmentPieceReader:
@@ -185,20 +217,24 @@ class SegmentPieceReader:
     only until the chunk holding the bytes it is asked for has arrived, so an
     upload starts after the first chunk, as the reference's per-stripe
     EncodedReader does (segmentupload/encode.go:39-75).  With hash_pieces the
-    piece hashes need whole pieces, so that form encodes the segment in one
-    call before any reader returns."""
+    same streamed call also hashes every piece chunk by chunk
+    (EC_FLAG_HASH_PIECES), as the reference hashes each piece through a
+    TeeReader while it streams (piecestore/upload.go:155,262-270):
+    piece_hash(num) waits only for the tree fold after the last chunk."""
 
     def __init__(self, segment, redundancy, hash_pieces: bool = False, chunk_stripes: int = 0):
         self.segment = segment  # bytes-like, numpy array, or PinnedBackend
         self.redundancy = redundancy
         self.hash_pieces = hash_pieces  # also compute every piece's BLAKE3 in the same engine call
         self.chunk_stripes = chunk_stripes  # streamed upload chunk (0: the library's growing chunks)
-        self._mu = threading.Lock()
+        self._mu = threading.RLock()  # (re-entered when a stream's __del__ runs under it)
         self._padded: Optional[np.ndarray] = None
         self._parity: Optional[PinnedHost] = None
         self._hashes: Optional[np.ndarray] = None
         self._upload = None  # ec_upload handle of the streamed encode
         self._bufs = []
+        self._streams = 0  # piece streams handed out and not yet closed
+        self._closing = False
         self.stripes = 0
 
     def _prepare(self):
@@ -226,15 +262,18 @@ class SegmentPieceReader:
             parity = pinned_pool.get((n - k) * stripes * ess)
             self._bufs.append(parity)
             ctx = rs.scheme.ctx if hasattr(rs, "scheme") else rs.ctx
-            if self.hash_pieces:  # parity + the BLAKE3 of all n pieces (piecestore/upload.go:155,270)
+            if self.hash_pieces and n == k:  # no parity to stream: hash the data pieces in one call
                 self._hashes = np.empty((n, 32), dtype=np.uint8)
                 rc = N.load().ec_encode_segments_host_hashed(ctx, padded.ptr, 1, stripes, parity.ptr,
                                                              self._hashes.ctypes.data, N.EC_FLAG_PARITY_ONLY)
                 _raise(None, rc)
             elif n > k:
+                # parity streamed chunk by chunk; with hash_pieces the BLAKE3 of all n pieces along
+                # with it (piecestore/upload.go:155,270)
                 h = ctypes.c_void_p()
-                rc = N.load().ec_upload_begin(ctx, padded.ptr, stripes, parity.ptr, N.EC_FLAG_PARITY_ONLY,
-                                              self.chunk_stripes, ctypes.byref(h))
+                flags = N.EC_FLAG_PARITY_ONLY | (N.EC_FLAG_HASH_PIECES if self.hash_pieces else 0)
+                rc = N.load().ec_upload_begin(ctx, padded.ptr, stripes, parity.ptr, flags, self.chunk_stripes,
+                                              ctypes.byref(h))
                 _raise(None, rc)
                 self._upload = h
             self.stripes = stripes
@@ -249,12 +288,25 @@ class SegmentPieceReader:
         if num >= n:
             raise InfectiousError(f"num must be less than {n}")
         self._prepare()
-        if num < k:  # EncodeSingle of a data share is the share itself (rs.go:21-23)
-            return _DataPieceStream(self._padded, num)
-        return _PieceStream(self._parity[num - k], self._wait if self._upload is not None else None)
+        with self._mu:
+            if self._closing or self._padded is None:
+                raise EEStreamError("piece reader used after close")
+            self._streams += 1
+            if num < k:  # EncodeSingle of a data share is the share itself (rs.go:21-23)
+                return _DataPieceStream(self._padded, num, owner=self)
+            return _PieceStream(self._parity[num - k], self._wait if self._upload is not None else None, owner=self)
+
+    def _stream_closed(self):
+        with self._mu:
+            self._streams -= 1
+            if not (self._closing and self._streams == 0):
+                return
+            rc = self._release_locked()
+        _raise(None, rc)
 
     def _wait(self, end: int):
-        """Block until bytes [0, end) of every parity piece are in host memory."""
+        """Block until bytes [0, end) of every parity piece are in host memory
+        (a stream being read holds the reader open: the handle stays valid)."""
         ess = self.redundancy.erasure_share_size()
         h = self._upload
         if h is None:
@@ -275,22 +327,44 @@ class SegmentPieceReader:
         if not 0 <= num < self.redundancy.total_count():
             raise InfectiousError(f"num must be less than {self.redundancy.total_count()}")
         self._prepare()
-        return self._hashes[num].tobytes()
+        with self._mu:
+            if self._hashes is None:
+                if self._upload is None:
+                    raise EEStreamError("piece reader used after close")
+                hashes = np.empty((self.redundancy.total_count(), 32), dtype=np.uint8)
+                _raise(None, N.load().ec_upload_hashes(self._upload, hashes.ctypes.data))
+                self._hashes = hashes
+            return self._hashes[num].tobytes()
+
+    def _release_locked(self) -> int:
+        """End the engine call and return the buffers to the pool (under _mu)."""
+        rc = 0
+        if self._upload is not None:  # the engine may still be writing the parity buffer
+            rc = N.load().ec_upload_end(self._upload)
+            self._upload = None
+        for b in self._bufs:
+            pinned_pool.put(b)
+        self._bufs = []
+        self._padded = self._parity = self._hashes = None
+        return rc
 
     def close(self):
-        rc = 0
+        """Close the reader; its buffers go back to the pool once every piece
+        stream it handed out is closed too (streams still being read keep them)."""
         with self._mu:
-            if self._upload is not None:  # the engine may still be writing the parity buffer
-                rc = N.load().ec_upload_end(self._upload)
-                self._upload = None
-            for b in self._bufs:
-                pinned_pool.put(b)
-            self._bufs = []
-            self._padded = self._parity = self._hashes = None
+            self._closing = True
+            if self._streams > 0:
+                return None
+            rc = self._release_locked()
         _raise(None, rc)
 
     def __del__(self):
+        # unreachable, and so is every stream it handed out (each holds the reader): nothing can
+        # read its buffers any more
         try:
-            self.close()
+            with self._mu:
+                self._closing = True
+                self._streams = 0
+                self._release_locked()
         except Exception:
             pass
