@@ -82,6 +82,9 @@ typedef struct ec_ctx ec_ctx;
 typedef void *ec_stream; /* hipStream_t; NULL = the default stream */
 
 int ec_create(int k, int n, int erasure_share_size, ec_ctx **out);
+/* Every streamed upload (ec_upload_begin) of the context must have ended
+ * (ec_upload_end) before ec_destroy; launches still queued on callers' streams
+ * are waited for. */
 void ec_destroy(ec_ctx *ctx);
 
 int ec_required(const ec_ctx *ctx);
@@ -298,6 +301,16 @@ int ec_gcm_seal_host(const uint8_t key[32], const uint8_t nonce[12], const uint8
                      size_t in_block, uint8_t *out);
 int ec_gcm_open_host(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *cipher, size_t nblocks,
                      size_t in_block, uint8_t *out, long long *bad_block);
+
+/* ---- on-box ceilings (the bench's roofline context; no reference counterpart) ----
+ * A plain streaming kernel, no arithmetic, in the read:write mix of an erasure
+ * kernel: each wave reads R KiB of src and writes W KiB to dst, one-shot grid,
+ * 16 B per lane per access (DESIGN.md §4 HBM table).  dst must hold
+ * read_bytes * W / R bytes.  *moved = the bytes read + written.  Async. */
+#define EC_PROBE_COPY 0       /* 1 : 1     (the rebuild) */
+#define EC_PROBE_ENCODE_MIX 1 /* 4 : 11    (the full encode's 29 : 80) */
+#define EC_PROBE_PARITY_MIX 2 /* 4 : 7     (the parity-only encode's 29 : 51) */
+int ec_bw_probe(int shape, const uint8_t *src, size_t read_bytes, uint8_t *dst, size_t *moved, ec_stream stream);
 
 /* ---- device helpers ---- */
 int ec_device_count(void);

@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "uplink_ec.h"
 
@@ -24,6 +25,15 @@ int or_baseline_encode_segment(int k, int n, int ess, const uint8_t *enc, const 
 void b3_hash(const uint8_t *in, size_t len, uint8_t out[32]);
 int64_t ag_encrypt_blocks(const uint8_t key[32], const uint8_t nonce[12], const uint8_t *plain, size_t nblocks,
                           size_t in_block, uint8_t *out, int threads);
+
+/* milliseconds since the start of main: every progress line is stamped, so a
+ * run stopped by a timeout names the phase it was in */
+static struct timespec t_start;
+static double ms(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (t.tv_sec - t_start.tv_sec) * 1e3 + (t.tv_nsec - t_start.tv_nsec) * 1e-6;
+}
 
 static int failures = 0;
 #define CHECK(cond, ...)                                                                                \
@@ -66,6 +76,7 @@ static void scheme_surface(int k, int n, int ess, int body) {
     uint8_t *in = malloc(stripe), *all = malloc((size_t)n * ess), *ref = malloc((size_t)n * ess);
     uint8_t *one = malloc(ess);
     fill(in, stripe);
+    printf("[%9.1f ms]   per-stripe encode\n", ms());
     CHECK(ec_encode(ctx, in, stripe, all) == EC_OK, "ec_encode");
     or_encode(k, n, enc, in, stripe, ref);
     CHECK(memcmp(all, ref, (size_t)n * ess) == 0, "ec_encode != oracle (%d,%d,%d)", k, n, ess);
@@ -87,6 +98,7 @@ static void scheme_surface(int k, int n, int ess, int body) {
     CHECK(strcmp(msg, want) == 0, "msg '%s' want '%s'", msg, want);
 
     /* Rebuild / Decode from the last k shares (all parity when n >= 2k) */
+    printf("[%9.1f ms]   per-stripe rebuild / decode\n", ms());
     int nums[256];
     const uint8_t *shp[256];
     uint8_t *shw[256];
@@ -131,6 +143,7 @@ static void scheme_surface(int k, int n, int ess, int body) {
     CHECK(rc == EC_ERR_NOT_ENOUGH_SHARES, "k-1 shares -> %d", rc);
 
     /* host-memory batch pipeline: 3 segments of 5 stripes */
+    printf("[%9.1f ms]   host pipeline\n", ms());
     const size_t nseg = 3, stripes = 5, spad = stripes * stripe, plen = stripes * (size_t)ess;
     uint8_t *segs = malloc(nseg * spad), *pieces = malloc(nseg * (size_t)n * plen), *pref = malloc((size_t)n * plen);
     uint8_t *back = malloc(nseg * spad);
@@ -151,6 +164,7 @@ static void scheme_surface(int k, int n, int ess, int body) {
 
     free(segs), free(pieces), free(pref), free(back);
     free(in), free(all), free(ref), free(one), free(out), free(out2), free(enc), free(vand), free(g);
+    printf("[%9.1f ms]   ec_destroy\n", ms());
     ec_destroy(ctx);
 }
 
@@ -188,8 +202,15 @@ static void adjacent_stages(void) {
     free(plain), free(ct), free(ref), free(back);
 }
 
-int main(void) {
+int main(int argc, char **argv) {
     setvbuf(stdout, NULL, _IONBF, 0); /* progress survives an abort */
+    clock_gettime(CLOCK_MONOTONIC, &t_start);
+    /* --build-id: which library this binary runs against, before any GPU work */
+    if (argc > 1 && strcmp(argv[1], "--build-id") == 0) {
+        printf("%s\n", ec_build_id());
+        return 0;
+    }
+    printf("[%9.1f ms] library build %s\n", ms(), ec_build_id());
     ec_ctx *bad = NULL;
     CHECK(ec_create(0, 4, 256, &bad) == EC_ERR_PARAMS, "k = 0");
     CHECK(ec_create(5, 4, 256, &bad) == EC_ERR_PARAMS, "k > n");
@@ -197,12 +218,13 @@ int main(void) {
     const int cfg[][3] = {{2, 4, 1024}, {4, 10, 256}, {29, 80, 256}, {20, 60, 4096}, {3, 7, 100}, {10, 20, 64}};
     for (size_t i = 0; i < sizeof cfg / sizeof cfg[0]; i++) {
         for (int body = EC_BODY_AUTO; body <= EC_BODY_STRAIGHT_LINE; body += EC_BODY_STRAIGHT_LINE) {
-            printf("RS(%d,%d) ess %d body %d\n", cfg[i][0], cfg[i][1], cfg[i][2], body);
+            printf("[%9.1f ms] RS(%d,%d) ess %d body %d\n", ms(), cfg[i][0], cfg[i][1], cfg[i][2], body);
             scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2], body);
         }
     }
-    printf("adjacent stages\n");
+    printf("[%9.1f ms] adjacent stages\n", ms());
     adjacent_stages();
+    printf("[%9.1f ms] returning from main (process exit follows)\n", ms());
     printf("%s: %d failures\n", failures ? "FAIL" : "ok", failures);
     return failures ? 1 : 0;
 }

@@ -18,10 +18,24 @@ def test_c_client_links_against_the_library():
     assert "libuplink_ec.so" in out and "not found" not in out
 
 
+def _run_client(binary, timeout=120):
+    """Run a C client with the library's diagnostic log on (UPLINK_EC_LOG: every
+    run-time compile and module load with its duration); on a timeout, fail with
+    everything it printed so far -- the client stamps each phase, so the last
+    line names where it stopped."""
+    env = dict(os.environ, UPLINK_EC_LOG="1")
+    try:
+        return subprocess.run([binary], capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired as e:
+        out = (e.stdout or b"").decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        err = (e.stderr or b"").decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        pytest.fail(f"{os.path.basename(binary)} timed out after {timeout} s; its output:\n{out}\n{err}")
+
+
 @pytest.mark.gpu
 def test_c_client_on_gpu():
     assert os.path.exists(BIN), "tests/c/build/abi_test missing: build() compiles it"
-    r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
+    r = _run_client(BIN)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().splitlines()[-1].startswith("ok")
 
@@ -30,9 +44,14 @@ def test_c_client_on_gpu():
 def test_c_client_on_gpu_checked_library():
     """The same client against libuplink_ec_checked.so, whose stripe kernels
     compare every global address with the launch's declared byte ranges and
-    trap (with the site printed) on one outside them."""
+    trap (with the site printed) on one outside them.  First, before any GPU
+    work, the two libraries must be one build (ec_build_id): a stale checked
+    library is reported as such instead of running."""
     assert os.path.exists(BIN_CHECKED), "tests/c/build/abi_test_checked missing: build() compiles it"
-    r = subprocess.run([BIN_CHECKED], capture_output=True, text=True, timeout=120)
+    ids = [subprocess.run([b, "--build-id"], capture_output=True, text=True, timeout=30).stdout.strip()
+           for b in (BIN, BIN_CHECKED)]
+    assert ids[0] and ids[0] == ids[1], f"checked library build {ids[1]} is not the product's {ids[0]}: rebuild both"
+    r = _run_client(BIN_CHECKED)
     assert "uplink_ec checked" not in r.stdout + r.stderr, r.stdout + r.stderr
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().splitlines()[-1].startswith("ok")

@@ -32,6 +32,8 @@ EC_FLAG_PARITY_ONLY = 0x1
 EC_FLAG_HASH_PIECES = 0x2
 # ec_set_body: body of the runtime-matrix kernel (include/uplink_ec.h)
 EC_BODY_AUTO, EC_BODY_JUMP_TABLE, EC_BODY_STRAIGHT_LINE = 0, 1, 2
+# ec_bw_probe shapes
+EC_PROBE_COPY, EC_PROBE_ENCODE_MIX, EC_PROBE_PARITY_MIX = 0, 1, 2
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 vp = ctypes.c_void_p
@@ -101,6 +103,7 @@ SIGNATURES = {
     "ec_upload_end": (ctypes.c_int, [vp]),
     "ec_host_alloc": (vp, [ctypes.c_size_t]),
     "ec_host_free": (None, [vp]),
+    "ec_bw_probe": (ctypes.c_int, [ctypes.c_int, vp, ctypes.c_size_t, vp, ctypes.POINTER(ctypes.c_size_t), vp]),
     "ec_device_count": (ctypes.c_int, []),
     "ec_set_device": (ctypes.c_int, [ctypes.c_int]),
     "ec_encode_kernel_name": (ctypes.c_char_p, [vp]),

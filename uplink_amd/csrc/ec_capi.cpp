@@ -24,6 +24,7 @@
 
 #include "../../include/uplink_ec.h"
 #include "blake3.hpp"
+#include "ec_log.hpp"
 #include "gf256.hpp"
 #include "rs_correct.hpp"
 #include "rs_kernels.hpp"
@@ -120,8 +121,16 @@ struct StreamMarks {
     uint64_t launched(hipStream_t s) {
         std::lock_guard<std::mutex> g(mu);
         Mark *m = nullptr;
-        for (auto &x : marks)
-            if (x.s == s) m = &x;
+        for (auto it = marks.begin(); it != marks.end(); ++it)
+            if (it->s == s) {
+                if (std::next(it) != marks.end()) {  // most recently used last: eviction takes the idlest
+                    Mark keep = *it;
+                    marks.erase(it);
+                    marks.push_back(keep);
+                }
+                m = &marks.back();
+                break;
+            }
         if (!m) {
             if (marks.size() >= kMaxStreams) {  // the least recently used stream's marks go
                 if (marks.front().ev) (void)hipEventDestroy(marks.front().ev);
@@ -692,10 +701,14 @@ void queue_done(ec_ctx *c, hipStream_t s, int slot, bool launched) {
     QueueRing &q = c->qring;
     std::lock_guard<std::mutex> g(q.mu);
     if (launched) {
+        // a slot's first launch for a stream that did not own it gets its event at once, so a
+        // stream that launches a few times and goes away (a stream per request) does not keep
+        // the slot from every other stream for good
+        const bool new_owner = !q.used[slot] || q.owner[slot] != s;
         q.used[slot] = true;
         q.owner[slot] = s;
         q.covered[slot] = false;
-        if (++q.since[slot] >= q.event_every) {
+        if (new_owner || ++q.since[slot] >= q.event_every) {
             q.since[slot] = 0;
             q.covered[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
         }
@@ -734,6 +747,7 @@ void ensure_sl(ec_ctx *c, MatPlan &plan) {
     const size_t used = sl::generate(plan.M.data(), plan.rows, plan.nin, code.data(), code.size(), offs);
     if (!used) return;  // does not fit
     size_t roff = 0, rwords = 0;
+    const double t0 = log_ms();
     std::vector<uint8_t> img = sl::template_image(used, &roff, &rwords);
     memcpy(img.data() + roff + 16, code.data() + 4, (used - 4) * 4);  // the marker words stay
     std::lock_guard<std::mutex> gs(c->setup_mu);
@@ -765,6 +779,8 @@ void ensure_sl(ec_ctx *c, MatPlan &plan) {
     plan.d_sl = d;
     plan.sl_bytes = dbytes;
     plan.sl_ready.store(true, std::memory_order_release);
+    ec_logf("straight-line module: %d rows x %d inputs, %zu words of code, made and loaded in %.1f ms", plan.rows,
+         plan.nin, used, log_ms() - t0);
 }
 
 // Launch the product described by `a` with the rows of `plan` (out_off gives

@@ -71,20 +71,22 @@ __device__ __forceinline__ void slice_inputs(const RsArgs &a, int64_t seg, const
 // ------------------------------------------------ runtime-matrix body
 // rs_jump_table.inc (tools/gen/gen_jump_table.py): 256 compile-time leaves,
 // leaf c = "acc[row] ^= c * x" as one v_bitop3 per plane from the 4-plane
-// XOR combinations lo[1..15] / hi[1..15] of the current input x.
+// XOR combinations lo[1..15] / hi[1..15] of the current input x, and the XORs
+// that make those combinations (RS_JT_COMBOS_ASM).
 #include "rs_jump_table.inc"
 
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
 // acc[O] ^= sum over the n inputs j of D[row O][j] * x_j, for the wave's
-// 8 - skip accumulator rows.  xa = LDS byte address of plane 0 of the first
-// input for this lane (plane p at +256 p, the next input 2 KiB on); tp = the
-// first input's 8 absolute leaf addresses of the wave's rows, right-aligned
+// 8 - skip accumulator rows.  xa = LDS byte address of the first input for
+// this lane in the wide layout (slice_inputs WIDE: planes 0-3 of the lane as
+// one 16-byte word at +0, planes 4-7 at +1024, the next input 2 KiB on); tp =
+// the first input's 8 absolute leaf addresses of the wave's rows, right-aligned
 // (entry skip + i holds row i), in global memory (rs_jt_targets), the next
 // input's `tstride` bytes on.  Per input, one scalar load brings the leaf
-// addresses straight into the call registers s[52:67] while the planes land
-// in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8]; 22 XORs fill the other
-// combinations; then, with VGPR index mode on for the accumulator operand
+// addresses straight into the call registers s[52:67] while two ds_read_b128
+// put the planes in the single-bit slots lo[1,2,4,8] / hi[1,2,4,8] (v[96:103]);
+// 22 XORs fill the other combinations; then, with VGPR index mode on for the accumulator operand
 // (SRC0 and DST, M0 = 8 * row, stepped by each leaf), a jump enters the
 // sequence of eight s_swappc_b64 (4 bytes each) at call site `skip`, so only
 // the wave's rows are visited; the leaves return with s_setpc_b64.  The loop
@@ -108,40 +110,13 @@ __device__ __forceinline__ void jt_inputs(u32x8 (&acc)[8], uint32_t xa, const ui
         "s_add_u32 s42, s42, .Ljt_sites%=-.Ljt_pc%=\n"
         "s_addc_u32 s43, s43, 0\n"
         ".Ljt_loop%=:\n"
-        "ds_read_b32 v96, %[xa]\n"
-        "ds_read_b32 v97, %[xa] offset:256\n"
-        "ds_read_b32 v99, %[xa] offset:512\n"
-        "ds_read_b32 v103, %[xa] offset:768\n"
-        "ds_read_b32 v111, %[xa] offset:1024\n"
-        "ds_read_b32 v112, %[xa] offset:1280\n"
-        "ds_read_b32 v114, %[xa] offset:1536\n"
-        "ds_read_b32 v118, %[xa] offset:1792\n"
+        "ds_read_b128 v[96:99], %[xa]\n"
+        "ds_read_b128 v[100:103], %[xa] offset:1024\n"
         "v_add_u32 %[xa], 0x800, %[xa]\n"
         "s_add_u32 %[off], %[off], %[ts]\n"
         "s_sub_u32 %[n], %[n], 1\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_xor_b32 v98, v96, v97\n"
-        "v_xor_b32 v100, v96, v99\n"
-        "v_xor_b32 v101, v97, v99\n"
-        "v_xor_b32 v102, v98, v99\n"
-        "v_xor_b32 v104, v96, v103\n"
-        "v_xor_b32 v105, v97, v103\n"
-        "v_xor_b32 v106, v98, v103\n"
-        "v_xor_b32 v107, v99, v103\n"
-        "v_xor_b32 v108, v100, v103\n"
-        "v_xor_b32 v109, v101, v103\n"
-        "v_xor_b32 v110, v102, v103\n"
-        "v_xor_b32 v113, v111, v112\n"
-        "v_xor_b32 v115, v111, v114\n"
-        "v_xor_b32 v116, v112, v114\n"
-        "v_xor_b32 v117, v113, v114\n"
-        "v_xor_b32 v119, v111, v118\n"
-        "v_xor_b32 v120, v112, v118\n"
-        "v_xor_b32 v121, v113, v118\n"
-        "v_xor_b32 v122, v114, v118\n"
-        "v_xor_b32 v123, v115, v118\n"
-        "v_xor_b32 v124, v116, v118\n"
-        "v_xor_b32 v125, v117, v118\n"
+        RS_JT_COMBOS_ASM
         "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)\n"
         "s_setpc_b64 s[42:43]\n"
         ".Ljt_sites%=:\n"

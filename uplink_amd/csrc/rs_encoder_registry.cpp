@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include "ec_log.hpp"
+
 #include <condition_variable>
 #include <cstdio>
 #include <dlfcn.h>
@@ -125,8 +127,11 @@ void join_compiles() {
         g_exiting = true;
         t.swap(g_threads);
     }
+    const double t0 = log_ms();
+    ec_logf("exit: joining %zu encoder compile thread(s)", t.size());
     for (auto &th : t)
         if (th.joinable()) th.join();
+    ec_logf("exit: compile threads joined after %.1f ms", log_ms() - t0);
 }
 
 // Load the compiler library hiprtc would load on its first compile, and keep it
@@ -143,15 +148,20 @@ std::string variant_expr(int k, int n, int nc, int nl, bool copy) {
 
 // Compile (or read from the cache) the two variants of (k, n) for `arch`.
 void compile_entry(JitEntry *e, std::string arch, int k, int n, bool read_cache) {
+    const double t_queued = log_ms();
     std::lock_guard<std::mutex> serial(g_compile_mu);
     {
         std::lock_guard<std::mutex> g(g_mu);
         if (g_exiting) {
+            ec_logf("RS(%d,%d) encoder compile skipped (exiting)", k, n);
             e->state = JitEntry::kFailed;
             g_cv.notify_all();
             return;
         }
     }
+    const double t_start = log_ms();
+    ec_logf("RS(%d,%d) encoder: start (%s, queued %.1f ms)", k, n, read_cache ? "cache allowed" : "no cache",
+         t_start - t_queued);
     const std::string src = "#include \"rs_encoder.hpp\"\n";
     const std::string full = variant_expr(k, n, enc::full_compute_waves(k, n), enc::full_loader_waves(k, n), true),
                       parity = variant_expr(k, n, enc::parity_compute_waves(k, n), enc::loader_waves(k, n), false);
@@ -183,6 +193,10 @@ void compile_entry(JitEntry *e, std::string arch, int k, int n, bool read_cache)
             (void)remove((path + ".co").c_str());
             (void)remove((path + ".names").c_str());
         }
+        ec_logf("RS(%d,%d) encoder: disk cache %s (%s)", k, n, code.empty() ? "miss" : "hit", path.c_str());
+    } else {
+        ec_logf("RS(%d,%d) encoder: disk cache not used (%s: %s)", k, n, dir.c_str(),
+             trusted ? "recompiling" : "not a private directory of this user");
     }
     if (code.empty()) {
         hiprtcProgram prog;
@@ -236,6 +250,8 @@ void compile_entry(JitEntry *e, std::string arch, int k, int n, bool read_cache)
             }
         }
     }
+    ec_logf("RS(%d,%d) encoder: %s after %.1f ms", k, n, code.empty() ? "FAILED" : "code object ready",
+         log_ms() - t_start);
     std::lock_guard<std::mutex> g(g_mu);
     if (code.empty()) {
         e->state = JitEntry::kFailed;

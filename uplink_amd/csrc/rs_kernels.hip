@@ -84,7 +84,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     const int npass = a.nout > 0 ? (a.nout + NW * OPW - 1) / (NW * OPW) : 1;
-    const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * (SL ? 16 : 4);
+    const uint32_t lds_addr = (uint32_t)(uintptr_t)lds + (uint32_t)lane * 16;  // the wide layout, both bodies
     // Plane chunks alternate between two LDS buffers, so one barrier per chunk
     // suffices: a wave staging chunk c+1 has passed barrier c, which every wave
     // reached only after it finished reading chunk c-1 from that buffer.
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
             load_inputs<NW, PER, true>(a, seg, c, wave, 0, a.nin < CH ? a.nin : CH, r);
             for (int j0 = 0; j0 < a.nin; j0 += CH) {
                 const int jn = a.nin - j0 < CH ? a.nin - j0 : CH;
-                slice_inputs<NW, PER, true, SL>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
+                slice_inputs<NW, PER, true, true>(a, seg, c, lds + buf * (JC * 8 * 64), lane, wave, j0, jn, pass == 0, r);
                 lds_barrier();
                 // the next chunk's loads are in flight while this chunk is multiplied in
                 if (j0 + CH < a.nin) {
@@ -156,8 +156,8 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_jt(const RsArgs a) {
 // rewrites column 0 with the bytes already there), so each wave's count of
 // VMEM operations is exact.  Each pass's pipeline starts and drains within
 // the pass.
-// SL = false: the same pipeline around the jump-table body (a plan's first
-// launch), its planes sliced into the narrow layout (plane p at 256 p + 4 lane).
+// SL = false: the same pipeline around the jump-table body (per-stripe calls,
+// or a plan before its generated code is ready), reading the same wide layout.
 template <int NW, int D, bool SL = true>
 __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
     constexpr int JC = SL ? sl::chunk_inputs(NW) : 2 * NW, PER = (JC + NW - 1) / NW, OPW = kJtRows, S = D + 1,
@@ -244,16 +244,9 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
                         }
                         uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
                         bitslice8(w);
-                        if constexpr (SL) {
-                            slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
-                            slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
-                        } else {
-                            // the wave read all of its input's raw bytes above (LDS operations of a
-                            // wave complete in order), so the narrow layout may overwrite them
-                            uint32_t *np = (uint32_t *)(slot + j * 128) + lane;
-#pragma unroll
-                            for (int q = 0; q < 8; q++) np[q * 64] = w[q];
-                        }
+                        // (in place: the wide layout both bodies read puts a lane's planes where its bytes were)
+                        slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
+                        slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
                     }
                 }
                 st2 = st1;
@@ -267,7 +260,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_dma(const RsArgs a) {
                                    a.jt_tgt + (pass * nchunks + ch) * NW + group);
                     } else {
                         const int jn = a.nin - j0 < CH ? a.nin - j0 : CH;
-                        jt_inputs(acc, ring_addr + (uint32_t)((ch % S) * SLOT) + (uint32_t)lane * 4,
+                        jt_inputs(acc, ring_addr + (uint32_t)((ch % S) * SLOT) + (uint32_t)lane * 16,
                                   a.jt_tgt + ((pass * a.nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
                                   (uint32_t)(OPW - cnt), (uint32_t)jn);
                     }

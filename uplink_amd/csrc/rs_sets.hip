@@ -227,18 +227,16 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
                         }
                         uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
                         bitslice8(w);
-                        // (all of the input's raw bytes were read above: LDS operations of a
-                        // wave complete in order, so the narrow layout may overwrite them)
-                        uint32_t *np = (uint32_t *)(slot + j * 128) + lane;
-#pragma unroll
-                        for (int q = 0; q < 8; q++) np[q * 64] = w[q];
+                        // in place, in the wide layout jt_inputs reads (a lane's planes where its bytes were)
+                        slot[j * 128 + lane] = (u32x4){w[0], w[1], w[2], w[3]};
+                        slot[j * 128 + 64 + lane] = (u32x4){w[4], w[5], w[6], w[7]};
                     }
                 }
                 lds_barrier();
                 if (ch + 1 < nchunks) issue(ch + 1);
                 if (cnt > 0) {
                     const int jn = nin - j0 < CH ? nin - j0 : CH;
-                    jt_inputs(acc, ring_addr + (uint32_t)((ch & 1) * SLOT) + (uint32_t)lane * 4,
+                    jt_inputs(acc, ring_addr + (uint32_t)((ch & 1) * SLOT) + (uint32_t)lane * 16,
                               d->tgt + ((pass * nin + j0) * NW + group) * OPW, (uint32_t)(NW * OPW * 8),
                               (uint32_t)(OPW - cnt), (uint32_t)jn);
                 }

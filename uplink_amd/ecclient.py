@@ -208,10 +208,15 @@ class ECClient:
         readers = streams.encode_reader2(streams.nop_closer(_BytesReader(padded)), rs)  # EncodeReader2 (:126)
 
         cancel = threading.Event()  # piecesCtx / piecesCancel (:139-140)
+        done = threading.Event()  # set on every way out of put (the watcher stops with it)
+        try:
+            return self._put_pieces(limits, rs, readers, cancel, parent, done, piece_count)
+        finally:
+            done.set()
+
+    def _put_pieces(self, limits, rs, readers, cancel, parent, done, piece_count):
         infos: List[Tuple[int, Optional[BaseException], object]] = []
         cv = threading.Condition()
-
-        done = threading.Event()
         if parent is not None:
             def watch():  # piecesCtx is a child of the caller's context (client.go:139)
                 while not done.is_set():
@@ -258,7 +263,6 @@ class ECClient:
                 cancel.set()  # cancelling remaining uploads (:178-181)
         for t in threads:
             t.join()
-        done.set()
         self.last_counts = {"total": piece_count, "optimal": rs.optimal_threshold(), "successful": successful,
                             "failed": failed, "canceled": canceled}
         joined = "; ".join(str(e) for e in errors)
