@@ -20,10 +20,14 @@ def test_c_client_links_against_the_library():
 
 def _run_client(binary, timeout=120):
     """Run a C client with the library's diagnostic log on (UPLINK_EC_LOG: every
-    run-time compile and module load with its duration); on a timeout, fail with
-    everything it printed so far -- the client stamps each phase, so the last
-    line names where it stopped."""
-    env = dict(os.environ, UPLINK_EC_LOG="1")
+    run-time compile and module load with its duration) and run-time encoder
+    compilation off (UPLINK_EC_JIT=0): its RS(10,20) per-stripe encodes would
+    start a hiprtc compile that process exit then waits for, minutes when the
+    box's disk cache is cold -- the checked client's round-2 and round-4
+    timeouts; the compile path has its own tests (exit_test).
+    On a timeout, fail with everything it printed so far: the client stamps
+    each phase, so the last line names where it stopped."""
+    env = dict(os.environ, UPLINK_EC_LOG="1", UPLINK_EC_JIT="0")
     try:
         return subprocess.run([binary], capture_output=True, text=True, timeout=timeout, env=env)
     except subprocess.TimeoutExpired as e:

@@ -214,3 +214,77 @@ def test_baseline_rebuild_matches(oracle):
         assert np.array_equal(out, seg)
         out2 = NP.rebuild_segment(f.enc, nums, [pieces[i] for i in nums], ess)
         assert np.array_equal(out2, seg)
+
+
+@pytest.mark.parametrize("k,n", [(1, 3), (4, 10), (20, 60), (29, 80), (100, 200)])
+def test_lagrange_decode_rows_equal_the_inversion(oracle, k, n):
+    """rs_sets_prep (uplink_amd/csrc/rs_sets.hip) computes each segment's decode
+    rows in closed form instead of inverting: G is the Lagrange basis on the
+    points x_0 = 0, x_i = alpha^(i-1), so the inverse of the k rows of the
+    chosen shares S is interpolation through S's points,
+        D[d][s] = N(x_d) / ((x_d ^ x_s) W_s),  N(y) = prod_t (y ^ x_t),
+        W_s = prod_{t != s} (x_s ^ x_t),
+    and a non-basis share u is predicted by the same formula at x_u.  Here: the
+    rows in that form equal the rows of the inverted chosen-rows matrix (the
+    oracle's G, infectious' share choice), and the prediction of every other
+    share equals G[u] times the inverse."""
+    exp = [0] * 512
+    log = [0] * 256
+    x = 1
+    for i in range(255):
+        exp[i] = exp[i + 255] = x
+        log[x] = i
+        x <<= 1
+        if x & 0x100:
+            x ^= 0x11D
+
+    def mul(a, b):
+        return 0 if a == 0 or b == 0 else exp[log[a] + log[b]]
+
+    def pt(r):
+        return 0 if r == 0 else exp[(r - 1) % 255]
+
+    def invert(m):
+        kk = len(m)
+        a = [list(row) + [int(i == j) for j in range(kk)] for i, row in enumerate(m)]
+        for c in range(kk):
+            p = next(r for r in range(c, kk) if a[r][c])
+            a[c], a[p] = a[p], a[c]
+            iv = exp[255 - log[a[c][c]]]
+            a[c] = [mul(iv, v) for v in a[c]]
+            for r in range(kk):
+                if r != c and a[r][c]:
+                    f = a[r][c]
+                    a[r] = [v ^ mul(f, w) for v, w in zip(a[r], a[c])]
+        return [row[kk:] for row in a]
+
+    G = oracle.FEC(k, n).enc.reshape(n, k).tolist()
+    rng = np.random.default_rng(k * 1000 + n)
+    for _ in range(2):
+        srt = sorted(rng.choice(n, k, replace=False).tolist())
+        b, e, ids = 0, k - 1, []
+        for i in range(k):  # infectious Rebuild's choice (front if its number is i, else back)
+            if srt[b] == i:
+                ids.append(srt[b])
+                b += 1
+            else:
+                ids.append(srt[e])
+                e -= 1
+        inv = invert([[int(j == i) for j in range(k)] if ids[i] < k else G[ids[i]] for i in range(k)])
+        xs = [pt(v) for v in ids]
+        lw = [sum(log[xs[p] ^ xs[t]] for t in range(k) if t != p) % 255 for p in range(k)]
+
+        def row_at(y):
+            ln = sum(log[y ^ xs[t]] for t in range(k)) % 255
+            return [exp[(ln - log[y ^ xs[j]] - lw[j]) % 255] for j in range(k)]
+        for d in range(k):
+            if ids[d] >= k:  # a missing data position
+                assert row_at(pt(d)) == inv[d], (k, n, d)
+        for u in rng.choice([v for v in range(n) if v not in ids], min(5, n - k), replace=False).tolist():
+            pred = [0] * k
+            for j in range(k):
+                acc = 0
+                for t in range(k):
+                    acc ^= mul(G[u][t], inv[t][j])
+                pred[j] = acc
+            assert row_at(pt(u)) == pred, (k, n, u)

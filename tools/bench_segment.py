@@ -39,10 +39,12 @@ def main():
     lib = NAT.load()
     res = {}
     for hashed in (False, True):
-        first, whole, hashes, blocking = [], [], [], []
+        first, whole, hashes, blocking, begin = [], [], [], [], []
         for it in range(12):
             spr = segment.SegmentPieceReader(be, rs, chunk_stripes=chunk, hash_pieces=hashed)
             t0 = time.perf_counter()
+            spr._prepare()  # pad + ec_upload_begin (everything queued)
+            tb = time.perf_counter()
             r = spr.piece_reader(K)
             b = r.read(4096)
             t1 = time.perf_counter()
@@ -72,13 +74,15 @@ def main():
                 whole.append(t2 - t0)
                 hashes.append(t3 - t0)
                 blocking.append(t5 - t4)
-        f, w, h, bl = (float(np.median(x)) for x in (first, whole, hashes, blocking))
+                begin.append(tb - t0)
+        f, w, h, bl, bg = (float(np.median(x)) for x in (first, whole, hashes, blocking, begin))
         res[hashed] = (f, w, h, bl)
         tag = "hash_pieces=True" if hashed else "no hashes"
         print(f"streamed upload, {tag} (chunk {'library default' if not chunk else chunk}): first parity byte after "
               f"{f * 1e3:.3f} ms ({100 * f / w:.1f} % of the segment), whole segment {w * 1e3:.2f} ms = "
               f"{SEG / w / 2**30:.2f} GiB/s payload, {(SEG + parity_bytes) / w / 1e9:.1f} GB/s PCIe"
-              + (f"; all piece hashes after {h * 1e3:.2f} ms" if hashed else ""))
+              + (f"; all piece hashes after {h * 1e3:.2f} ms" if hashed else "")
+              + f"; pad + ec_upload_begin returned after {bg * 1e3:.3f} ms")
         print(f"  blocking ec_encode_segments_host{'_hashed' if hashed else ''} (parity only): {bl * 1e3:.2f} ms = "
               f"{SEG / bl / 2**30:.2f} GiB/s payload; streamed / blocking whole-segment time {w / bl:.3f}")
     print(f"hashed / unhashed streamed: first byte {res[True][0] / res[False][0]:.3f}, whole segment "

@@ -393,6 +393,10 @@ struct ec_ctx {
     int fault_max_batch = 0, fault_fail_num = -1;
     // share-set calls (ec_*_segments_sets, and fresh share sets of the batched rebuild)
     uint64_t jt_base = 0;          // address of the jump table's leaf 0 on this device
+    // one launch per share-set call on the widest class's waves, instead of one per wave-count
+    // class: 951.2 vs 982.6 us per 32 fresh-set segments on one box (profiles/r05/d/bench_sets*.json);
+    // UPLINK_EC_SETS_MERGE=0 at ec_create for the per-class launches (A/B)
+    bool sets_merge = true;
     SetsRing sets;
     SlBuilder slb;
 };
@@ -1055,6 +1059,11 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     const int k = c->k, ess = c->ess;
     const size_t nseg = segs.size();
     if (nseg == 0 || nstripes == 0) return EC_OK;
+    if (c->sets_merge) {  // every segment on the widest class's workgroups: one launch, one tail
+        int nw = 2;
+        for (auto &sg : segs) nw = std::max(nw, sg.nw);
+        for (auto &sg : segs) sg.nw = nw;
+    }
     std::vector<int> idx(nseg);
     for (size_t g = 0; g < nseg; g++) idx[g] = (int)g;
     std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return segs[x].nw < segs[y].nw; });
@@ -1062,7 +1071,7 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     size_t words = 0;
     for (size_t q = 0; q < nseg; q++) {
         toff[q] = words;
-        words += (sets_tgt_entries(segs[idx[q]].nin, segs[idx[q]].rows) + 7) & ~(size_t)7;
+        words += (sets_tgt_entries(segs[idx[q]].nin, segs[idx[q]].rows, segs[idx[q]].nw) + 7) & ~(size_t)7;
     }
     SetsSlot *sl = sets_acquire(c, nseg, words);
     if (!sl) return EC_ERR_DEVICE;
@@ -1326,6 +1335,7 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     HIP_TRY(hipMemset(c->d_chk, 0, 4));
 #endif
     if (const char *e = getenv("UPLINK_EC_QUEUE_EVENT_EVERY")) c->qring.event_every = std::max(1, atoi(e));
+    if (const char *e = getenv("UPLINK_EC_SETS_MERGE")) c->sets_merge = atoi(e) != 0;
     configure_rebuild(getenv("UPLINK_EC_REBUILD_DEPTH") ? atoi(getenv("UPLINK_EC_REBUILD_DEPTH")) : 1);
     if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
         if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;
@@ -2041,6 +2051,16 @@ struct ec_upload {
     std::atomic<int> rc{EC_OK};
     std::atomic<int> done{0};  // leading chunks known to be in host memory
     int n = 0;                 // pieces hashed (EC_FLAG_HASH_PIECES), 0 without
+    // the hash work, queued by the first caller that waits on the upload or asks for the hashes
+    // (not by ec_upload_begin, so the first chunk's copies and encode start without waiting for
+    // the host to queue ~10 more operations)
+    std::once_flag hash_once;
+    int hash_rc = EC_OK;
+    bool streamed_hash = false, parity_only = false;
+    size_t nstripes = 0;
+    B3View dv{}, pv{};
+    uint32_t *cvs = nullptr;
+    uint8_t *d_hashes = nullptr, *d_scratch = nullptr, *d_parity = nullptr;
     // ec_upload_end waits for the callers inside ec_upload_wait / _ready /
     // _hashes before it frees the handle (piece readers block in
     // those while another thread closes the segment)
@@ -2164,7 +2184,7 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         sl.ev.push_back(e);
     }
-    hipStream_t h2d = sl.st[0], comp = sl.st[1], d2h = sl.st[2], hs = sl.st[3];
+    hipStream_t h2d = sl.st[0], comp = sl.st[1], d2h = sl.st[2];
     uint32_t *cvs = (uint32_t *)sl.d_hash;
     uint8_t *d_hashes = sl.d_hash + cvs_bytes, *d_scratch = d_hashes + hash_bytes;
     const uint8_t *d_parity = sl.d_out + (parity_only ? 0 : (size_t)c->k * plen);
@@ -2188,24 +2208,18 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
                                           hipMemcpyDeviceToHost, d2h) != hipSuccess) ||
             hipEventRecord(e_out, d2h) != hipSuccess)
             rc = EC_ERR_DEVICE;
-        // this chunk's BLAKE3 chunks of every piece, off the encode's critical path
-        if (rc == EC_OK && streamed_hash) {
-            const uint64_t c0 = s0 * ess / 1024, c1 = ch + 1 == nch ? nb3 : s1 * ess / 1024;
-            if (hipStreamWaitEvent(hs, e_enc, 0) != hipSuccess ||
-                b3_launch_chunk_range(dv, pv, c0, c1, cvs, hs) != hipSuccess)
-                rc = EC_ERR_DEVICE;
-        }
     }
-    if (rc == EC_OK && hashed) {
-        hipError_t e = hipStreamWaitEvent(hs, sl.ev[2 * nch - 1], 0);  // (the last encode)
-        if (e == hipSuccess)
-            e = streamed_hash ? b3_launch_fold(cvs, c->n, nb3, d_hashes, d_scratch, hs)
-                              : (hash_segments(c, sl.d_in, d_parity, 1, nstripes, d_hashes, d_scratch, hs) == EC_OK
-                                     ? hipSuccess : hipErrorUnknown);
-        if (e == hipSuccess) e = hipMemcpyAsync(sl.h_hash, d_hashes, 32 * (size_t)c->n, hipMemcpyDeviceToHost, hs);
-        if (e == hipSuccess) e = hipEventRecord(sl.ev[3 * nch], hs);
-        if (e != hipSuccess) rc = hip_fail(e);
+    if (hashed) {  // queued later (upload_queue_hashes): the first chunk is not held up by it
         u->n = c->n;
+        u->streamed_hash = streamed_hash;
+        u->parity_only = parity_only;
+        u->nstripes = nstripes;
+        u->dv = dv;
+        u->pv = pv;
+        u->cvs = cvs;
+        u->d_hashes = d_hashes;
+        u->d_scratch = d_scratch;
+        u->d_parity = (uint8_t *)d_parity;
     }
     u->rc.store(rc);
     if (rc) {
@@ -2214,6 +2228,41 @@ int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8
     }
     *out = u.release();
     return EC_OK;
+}
+
+// The piece-hash work of an EC_FLAG_HASH_PIECES upload, on its hash stream:
+// each group of about a third of the chunks hashed as soon as its last chunk
+// is encoded (a stream wait on that chunk's encode event), then the tree fold
+// and the hashes' copy to pinned memory.  Queued once, by the first caller of
+// ec_upload_wait or ec_upload_hashes.
+static void upload_queue_hashes(ec_upload *u) {
+    std::call_once(u->hash_once, [u] {
+        ec_ctx *c = u->c;
+        UploadSlot &sl = *u->slot;
+        const size_t nch = u->end.size(), ess = c->ess;
+        const uint64_t nb3 = (u->nstripes * ess + 1023) / 1024;
+        hipStream_t hs = sl.st[3];
+        hipError_t e = hipSuccess;
+        if (u->streamed_hash) {
+            size_t from = 0;  // first stripe not yet hashed
+            for (size_t ch = 0; ch < nch && e == hipSuccess; ch++) {
+                const bool last = ch + 1 == nch;
+                if (!last && (u->end[ch] - from) * 3 < u->nstripes) continue;  // (groups of ~1/3 of the segment)
+                const uint64_t c0 = from * ess / 1024, c1 = last ? nb3 : u->end[ch] * ess / 1024;
+                e = hipStreamWaitEvent(hs, sl.ev[nch + ch], 0);
+                if (e == hipSuccess) e = b3_launch_chunk_range(u->dv, u->pv, c0, c1, u->cvs, hs);
+                from = u->end[ch];
+            }
+        }
+        if (e == hipSuccess) e = hipStreamWaitEvent(hs, sl.ev[2 * nch - 1], 0);  // (the last encode)
+        if (e == hipSuccess)
+            e = u->streamed_hash ? b3_launch_fold(u->cvs, c->n, nb3, u->d_hashes, u->d_scratch, hs)
+                                 : (hash_segments(c, sl.d_in, u->d_parity, 1, u->nstripes, u->d_hashes, u->d_scratch,
+                                                  hs) == EC_OK ? hipSuccess : hipErrorUnknown);
+        if (e == hipSuccess) e = hipMemcpyAsync(sl.h_hash, u->d_hashes, 32 * (size_t)c->n, hipMemcpyDeviceToHost, hs);
+        if (e == hipSuccess) e = hipEventRecord(sl.ev[3 * nch], hs);
+        u->hash_rc = e == hipSuccess ? EC_OK : hip_fail(e);
+    });
 }
 
 static int upload_wait_chunks(ec_upload *u, size_t stripes) {
@@ -2237,6 +2286,7 @@ int ec_upload_wait(ec_upload *u, size_t stripes) {
     UploadUse use(u);
     if (!use.ok) return EC_ERR_INVALID_ARG;
     DeviceGuard dg(u->c->device);
+    if (u->n && u->rc.load() == EC_OK) upload_queue_hashes(u);  // (while the first chunk is on its way)
     return upload_wait_chunks(u, stripes);
 }
 
@@ -2258,6 +2308,8 @@ int ec_upload_hashes(ec_upload *u, uint8_t *hashes) {
     if (!use.ok || u->n == 0) return EC_ERR_INVALID_ARG;  // (begun without EC_FLAG_HASH_PIECES)
     if (const int rc = u->rc.load()) return rc;
     DeviceGuard dg(u->c->device);
+    upload_queue_hashes(u);
+    if (u->hash_rc) return u->hash_rc;
     if (hipEventSynchronize(u->slot->ev[3 * u->end.size()]) != hipSuccess) return EC_ERR_DEVICE;
     memcpy(hashes, u->slot->h_hash, 32 * (size_t)u->n);
     return EC_OK;

@@ -344,9 +344,22 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
 // faster and takes a minute of hiprtc time.
 constexpr int kJitMaxK = 48;
 
+// UPLINK_EC_JIT=0: no run-time compilation at all (library-built encoders and
+// the runtime-matrix kernel only).  A process that starts a compile waits for
+// it at exit (join_compiles), and a cold compile takes minutes on a box's CPU
+// share: the plain-C ABI client sets this (tests/test_c_abi.py), since its
+// RS(10,20) per-stripe encodes would otherwise start one.
+bool jit_allowed() {
+    static const bool on = [] {
+        const char *e = getenv("UPLINK_EC_JIT");
+        return !(e && e[0] == '0' && e[1] == 0);
+    }();
+    return on;
+}
+
 const EncoderKernel *find_encoder(int k, int n, bool wait) {
     if (const EncoderKernel *e = aot_encoder(k, n)) return e;
-    if (!enc::supported(k, n) || k > kJitMaxK) return nullptr;
+    if (!enc::supported(k, n) || k > kJitMaxK || !jit_allowed()) return nullptr;
     return jit_encoder(k, n, wait);
 }
 

@@ -291,8 +291,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
 
 int sets_waves(int rows) { return rows <= 16 ? 2 : rows <= 24 ? 3 : 4; }
 
-size_t sets_tgt_entries(int nin, int rows) {
-    const int nw = sets_waves(rows);
+size_t sets_tgt_entries(int nin, int rows, int nw) {
     const int npass = rows > 0 ? (rows + nw * kRows - 1) / (nw * kRows) : 1;
     return (size_t)npass * nin * nw * kRows;
 }

@@ -60,7 +60,7 @@ constexpr int64_t kTileChunksHost = 128;  // 16-byte chunks per tile (rs_tile.hp
 // waves per workgroup for `rows` computed rows (the jump-table body's split,
 // rs_kernels.hip jt_waves: <= 16 -> 2, <= 24 -> 3, else 4, 8 rows per wave)
 int sets_waves(int rows);
-size_t sets_tgt_entries(int nin, int rows);  // 64-bit words of one segment's leaf table
+size_t sets_tgt_entries(int nin, int rows, int nw);  // 64-bit words of one segment's leaf table on nw waves
 // one workgroup per segment; jt_base = address of leaf 0 (jt_table_base_addr);
 // zeroes *done_ctr for the launches that follow
 hipError_t launch_sets_prep(const SetStage *stage, SetDesc *desc, int nseg, uint64_t jt_base, uint32_t *done_ctr,
