@@ -54,15 +54,23 @@ def main():
     def fresh(count):
         return [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(count)]
 
-    def sets_call(sets, out=outs):
+    def sets_args(sets, out=outs):
+        """the call's ctypes arrays, made ahead of the timed calls (a Go caller has its slices)"""
         n = len(sets)
         nsh = (ctypes.c_int * n)(*[K] * n)
         flat = [x for s in sets for x in s]
         nums = (ctypes.c_int * len(flat))(*flat)
         ptrs = (ctypes.c_void_p * len(flat))(*[pcs[g].data_ptr() + x * PLEN for g, s in enumerate(sets) for x in s])
         optr = (ctypes.c_void_p * n)(*[out[g].data_ptr() for g in range(n)])
+        return n, nsh, nums, ptrs, optr
+
+    def sets_go(a):
+        n, nsh, nums, ptrs, optr = a
         rc = L.ec_rebuild_segments_sets(ctx, n, nsh, nums, ptrs, NSTRIPES, optr, sptr)
         assert rc == 0, _native.strerror(rc)
+
+    def sets_call(sets, out=outs):
+        sets_go(sets_args(sets, out))
 
     res = {}
     # warm-up (kernels loaded, slots allocated)
@@ -80,10 +88,11 @@ def main():
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
     all_sets = [fresh(nseg) for _ in range(args.reps)]
+    all_args = [sets_args(x) for x in all_sets]
     ev[0].record(st)
     t0 = time.perf_counter()
     for i in range(args.reps):
-        sets_call(all_sets[i])
+        sets_go(all_args[i])
         ev[i + 1].record(st)
     ev[-1].synchronize()
     wall = (time.perf_counter() - t0) / args.reps
@@ -95,21 +104,60 @@ def main():
                     "us_per_segment": round(t / nseg * 1e6, 2), "GBps": round(alg / t / 1e9, 1),
                     "frac": round(alg / t / 1e9 / PEAK, 4), "wall_us_per_call": round(wall * 1e6, 1),
                     "m_of_sets": sorted(int(sum(1 for x in s if x >= K)) for s in all_sets[0])}
+    # host time of one 32-segment call (the launch call alone, the ring empty)
+    host = []
+    for a in [sets_args(fresh(nseg)) for _ in range(6)]:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sets_go(a)
+        host.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    res["batch"]["host_us_per_call_median"] = round(float(np.median(host)) * 1e6, 1)
+    # the same 32 segments from ONE share set, warm plan, back to back on the stream: the
+    # straight-line body and the jump-table body of ec_rebuild_segments_batched, timed as above
+    one = all_sets[0][0]
+    cn = (ctypes.c_int * K)(*one)
+    cp = (ctypes.c_void_p * K)(*[pcs[0].data_ptr() + x * PLEN for x in one])
+    assert L.ec_prepare_rebuild(ctx, K, cn, 1) == 1
+    for body, name in ((_native.EC_BODY_AUTO, "straight_line"), (_native.EC_BODY_JUMP_TABLE, "jump_table")):
+        assert L.ec_set_body(ctx, body) == 0
+
+        def one_set():
+            assert L.ec_rebuild_segments_batched(ctx, K, cn, cp, NSTRIPES, nseg, N * PLEN, SPAD, outs.data_ptr(),
+                                                 sptr) == 0
+        for _ in range(3):
+            one_set()
+        torch.cuda.synchronize()
+        t_end = time.perf_counter() + 0.3
+        while time.perf_counter() < t_end:
+            one_set()
+        torch.cuda.synchronize()
+        ev[0].record(st)
+        for i in range(args.reps):
+            one_set()
+            ev[i + 1].record(st)
+        ev[-1].synchronize()
+        per1 = [ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(args.reps)]
+        t1 = float(np.median(per1))
+        res[f"one_set_{name}"] = {"m": int(sum(1 for x in one if x >= K)), "us_per_call_median": round(t1 * 1e6, 1),
+                                  "frac": round(alg / t1 / 1e9 / PEAK, 4), "body": int(L.ec_last_body(ctx))}
+    assert L.ec_set_body(ctx, _native.EC_BODY_AUTO) == 0
+    torch.cuda.synchronize()
     # single segment, fresh set, synchronous wall clock
     walls = []
     for i in range(args.reps * 4):
-        s1 = fresh(1)
+        a1 = sets_args(fresh(1), outs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        sets_call(s1, outs)
+        sets_go(a1)
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t0)
     ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    s1s = [fresh(1) for _ in range(args.reps)]
+    s1s = [sets_args(fresh(1), outs) for _ in range(args.reps)]
     torch.cuda.synchronize()
     ev2[0].record(st)
-    for s1 in s1s:
-        sets_call(s1, outs)
+    for a1 in s1s:
+        sets_go(a1)
     ev2[1].record(st)
     ev2[1].synchronize()
     b2b = ev2[0].elapsed_time(ev2[1]) * 1e-3 / args.reps

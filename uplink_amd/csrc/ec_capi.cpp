@@ -294,7 +294,8 @@ struct UploadSlot {
 // nor the prep kernel's ever overtake a launch still reading the slot, and no
 // event, marker or synchronisation is put on the caller's stream.
 struct SetsSlot {
-    SetStage *h_stage = nullptr;  // pinned, stage_cap entries
+    SetStage *h_stage = nullptr;  // pinned, stage_cap entries (host-cached unless the zero-copy form)
+    SetStage *d_stage = nullptr;  // device copy of it (the DMA form: one hipMemcpyAsync per call)
     size_t stage_cap = 0;
     SetDesc *d_desc = nullptr;    // device, stage_cap entries
     uint64_t *d_tgt = nullptr;    // device leaf tables, tgt_cap words
@@ -306,6 +307,7 @@ struct SetsSlot {
     bool dead = false;            // a launch failed after the prep: never reused
     ~SetsSlot() {
         if (h_stage) (void)hipHostFree(h_stage);
+        if (d_stage) (void)hipFree(d_stage);
         if (d_desc) (void)hipFree(d_desc);
         if (d_tgt) (void)hipFree(d_tgt);
         if (d_words) (void)hipFree(d_words);
@@ -397,6 +399,11 @@ struct ec_ctx {
     // class: 951.2 vs 982.6 us per 32 fresh-set segments on one box (profiles/r05/d/bench_sets*.json);
     // UPLINK_EC_SETS_MERGE=0 at ec_create for the per-class launches (A/B)
     bool sets_merge = true;
+    // the per-segment staging is read by the prep kernel straight from coherent pinned memory, or
+    // -- UPLINK_EC_SETS_STAGE_DMA=1 -- reaches the GPU by one DMA into device memory per call (host
+    // writes to cached pinned memory; the stream then waits ~20 us for the copy engine between
+    // calls, profiles/r05/g)
+    bool sets_stage_dma = false;
     SetsRing sets;
     SlBuilder slb;
 };
@@ -1015,10 +1022,13 @@ SetsSlot *sets_acquire(ec_ctx *c, size_t nseg, size_t tgt_words) {
     if (sl->stage_cap < nseg) {
         const size_t cap = std::max<size_t>(32, (nseg + 31) & ~(size_t)31);
         if (sl->h_stage) (void)hipHostFree(sl->h_stage);
+        if (sl->d_stage) (void)hipFree(sl->d_stage);
         if (sl->d_desc) (void)hipFree(sl->d_desc);
         if (sl->d_words) (void)hipFree(sl->d_words);
-        sl->h_stage = nullptr, sl->d_desc = nullptr, sl->d_words = nullptr;
-        ok = hipHostMalloc((void **)&sl->h_stage, cap * sizeof(SetStage), kSetsHostFlags) == hipSuccess &&
+        sl->h_stage = nullptr, sl->d_stage = nullptr, sl->d_desc = nullptr, sl->d_words = nullptr;
+        ok = hipHostMalloc((void **)&sl->h_stage, cap * sizeof(SetStage),
+                           c->sets_stage_dma ? hipHostMallocDefault : kSetsHostFlags) == hipSuccess &&
+             (!c->sets_stage_dma || hipMalloc(&sl->d_stage, cap * sizeof(SetStage)) == hipSuccess) &&
              hipMalloc(&sl->d_desc, cap * sizeof(SetDesc)) == hipSuccess &&
              hipMalloc(&sl->d_words, 4 * (cap + 1)) == hipSuccess;
         if (ok && cap + 1 > 65) {
@@ -1100,7 +1110,12 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     }
     const uint32_t seq = sl->seq + 1;
     const int64_t chunks = nstripes * (ess / 16), tiles = (chunks + kTileChunksHost - 1) / kTileChunksHost;
-    hipError_t e = launch_sets_prep(sl->h_stage, sl->d_desc, (int)nseg, c->jt_base, sl->d_words, s);
+    hipError_t e = hipSuccess;
+    if (sl->d_stage)  // (the host's writes went to cached memory; one DMA takes them to the device)
+        e = hipMemcpyAsync(sl->d_stage, sl->h_stage, nseg * sizeof(SetStage), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = launch_sets_prep(sl->d_stage ? sl->d_stage : sl->h_stage, sl->d_desc, (int)nseg, c->jt_base, sl->d_words,
+                             s);
     if (e != hipSuccess) {  // nothing was queued: the slot is as it was
         sets_release(c, sl);
         return hip_fail(e);
@@ -1336,6 +1351,7 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
 #endif
     if (const char *e = getenv("UPLINK_EC_QUEUE_EVENT_EVERY")) c->qring.event_every = std::max(1, atoi(e));
     if (const char *e = getenv("UPLINK_EC_SETS_MERGE")) c->sets_merge = atoi(e) != 0;
+    if (const char *e = getenv("UPLINK_EC_SETS_STAGE_DMA")) c->sets_stage_dma = atoi(e) != 0;
     configure_rebuild(getenv("UPLINK_EC_REBUILD_DEPTH") ? atoi(getenv("UPLINK_EC_REBUILD_DEPTH")) : 1);
     if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
         if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;

@@ -4,7 +4,8 @@
 // several at once under prefetch, private/storage/streams/store.go:240-253).
 //
 // Nothing is prepared on the host beyond the share choice: per segment the
-// host writes a SetStage into pinned memory; one launch of rs_sets_prep (one
+// host writes a SetStage into pinned memory (one DMA takes the call's records
+// to device memory); one launch of rs_sets_prep (one
 // workgroup per segment) copies its descriptor to the device, computes the
 // segment's decode rows (Lagrange interpolation weights, closed form) and
 // writes the jump-table leaf addresses of those rows; then rs_matmul_sets<NW> rebuilds every
@@ -28,7 +29,7 @@ struct SetDesc {
 };
 static_assert(sizeof(SetDesc) % 8 == 0, "copied as 8-byte words");
 
-// What the host writes per segment (pinned memory, read once by rs_sets_prep).
+// What the host writes per segment (pinned memory, copied to the device, read once by rs_sets_prep).
 // Inputs are the k basis shares (infectious' choice, position p holds share
 // num[p]; a present data share d sits at position d) followed by the other
 // shares (Decode).  Rows: the nstore missing data positions missing[r], then

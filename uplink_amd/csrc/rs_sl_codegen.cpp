@@ -9,6 +9,7 @@
 //   v_xor_b32_e32  vD, vA, vB            4-plane combinations; single-combination rows
 //   v_bitop3_b32   vD, vD, vL, vH 0x96   acc ^= lo[L] ^ hi[H]
 //   s_setpc_b64    s[48:49]              return to the calling kernel
+#include <stdlib.h>
 #include <string.h>
 
 #include "gf256_field.hpp"
@@ -150,7 +151,13 @@ Split split_for(int rows) {
 #ifndef UPLINK_SL_WIDE_ROWS_PER_WAVE  // rows per wave past 32 rows (at most kRows)
 #define UPLINK_SL_WIDE_ROWS_PER_WAVE 4
 #endif
-    constexpr int RW = UPLINK_SL_WIDE_ROWS_PER_WAVE;
+    // (the env var of the same name overrides it for A/B runs; read once, so the
+    // generated code and the launches of a process always agree)
+    static const int RW = [] {
+        const char *e = getenv("UPLINK_SL_WIDE_ROWS_PER_WAVE");
+        const int v = e ? atoi(e) : UPLINK_SL_WIDE_ROWS_PER_WAVE;
+        return v >= 4 && v <= kRows ? v : UPLINK_SL_WIDE_ROWS_PER_WAVE;
+    }();
     s.nw = rows <= UPLINK_SL_TWO_WAVE_ROWS ? 2
            : rows <= 3 * kRows                ? 3
            : rows <= 4 * kRows                ? 4
