@@ -424,7 +424,7 @@ def on_box_ceilings(L, dev, stream, read_bytes: int = 1 << 30, reps: int = 10):
     return out
 
 
-def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 10):
+def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 16):
     """The decode the way uplink runs it: every segment of a
     download is rebuilt from whichever 29 pieces answered first
     (private/eestream/stripe.go:314-354), so each brings a share set of its own
@@ -464,11 +464,17 @@ def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 10):
     call(fresh(nb))
     torch.cuda.synchronize(dev)
     ok = bool(torch.equal(outs, segs))
-    t_end = time.perf_counter() + 0.2  # clock settle
-    while time.perf_counter() < t_end:
-        call(fresh(nb))
     all_sets = [fresh(nb) for _ in range(reps)]
     all_args = [prep(x) for x in all_sets]
+    # clock settle at the timed loop's duty cycle (calls back to back, arrays made
+    # beforehand): a settle loop that builds its arrays in Python leaves the GPU idle
+    # between calls, and the first timed calls then run at a clock the steady state
+    # does not keep (816-838 us, then 930-1150, profiles/r05/h)
+    t_end = time.perf_counter() + 0.3
+    i = 0
+    while time.perf_counter() < t_end:
+        go(all_args[i % reps])
+        i += 1
     torch.cuda.synchronize(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     ev[0].record(stream)

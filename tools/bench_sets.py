@@ -34,7 +34,7 @@ PEAK = 8000.0
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=12)
+    ap.add_argument("--reps", type=int, default=24)
     ap.add_argument("--nseg", type=int, default=32)
     args = ap.parse_args()
     torch.cuda.set_device(0)
@@ -82,13 +82,16 @@ def main():
     torch.cuda.synchronize()
     ok = bool(torch.equal(outs, segs))
     # batch: back to back, events around each call
-    t_end = time.perf_counter() + 0.3
-    while time.perf_counter() < t_end:  # clock settle
-        sets_call(fresh(nseg))
-    torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
     all_sets = [fresh(nseg) for _ in range(args.reps)]
     all_args = [sets_args(x) for x in all_sets]
+    # clock settle at the timed loop's duty cycle (arrays made beforehand, calls back to back)
+    t_end = time.perf_counter() + 0.3
+    i = 0
+    while time.perf_counter() < t_end:
+        sets_go(all_args[i % args.reps])
+        i += 1
+    torch.cuda.synchronize()
     ev[0].record(st)
     t0 = time.perf_counter()
     for i in range(args.reps):
