@@ -273,7 +273,7 @@ def other_configs(L, dev, sptr, reps: int = 10):
     return out
 
 
-def decode_with_detection(L, dev, sptr, reps: int = 4, nb: int = 16):
+def decode_with_detection(L, dev, sptr, reps: int = 4, nb: int = 16, extras=(1, 4, 10, 20)):
     """Informational, outside the timed region: Decode with error detection on
     whole RS(29,80) 64 MiB segments, nb per call (ec_decode_segments_batched:
     syndrome rows checked for zero in the kernel, then Rebuild) from
@@ -294,7 +294,7 @@ def decode_with_detection(L, dev, sptr, reps: int = 4, nb: int = 16):
     rng = np.random.default_rng(616)
     res = {}
     ok = True
-    for extra in (1, 4, 10, 20):
+    for extra in extras:
         sets = [[int(x) for x in rng.permutation(N)[:K + extra]] for _ in range(4)]
         args = [((ctypes.c_int * len(s))(*s), (ctypes.c_void_p * len(s))(*[pcs.data_ptr() + i * plen for i in s]))
                 for s in sets]

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the straight-line split past 32 rows (UPLINK_SL_WIDE_ROWS_PER_WAVE,
 read once per process): Decode with detection at k+1..k+20 on whole RS(29,80)
-64 MiB segments, bench.py's informational leg.  Run once per setting."""
+64 MiB segments, bench.py's informational leg.  Run once per setting;
+args: the extra-share counts (default 1 4 10 20)."""
 import ctypes
 import json
 import os
@@ -15,6 +16,7 @@ from uplink_amd import _native  # noqa: E402
 
 torch.cuda.set_device(0)
 L = _native.load()
-res = bench.decode_with_detection(L, torch.device("cuda", 0), torch.cuda.current_stream().cuda_stream)
+extras = tuple(int(x) for x in sys.argv[1:]) or (1, 4, 10, 20)
+res = bench.decode_with_detection(L, torch.device("cuda", 0), torch.cuda.current_stream().cuda_stream, extras=extras)
 print(json.dumps({"rows_per_wave": os.environ.get("UPLINK_SL_WIDE_ROWS_PER_WAVE", "default"),
                   **{k: v for k, v in res.items() if k != "note"}}))
