@@ -1074,6 +1074,21 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
         for (auto &sg : segs) nw = std::max(nw, sg.nw);
         for (auto &sg : segs) sg.nw = nw;
     }
+    {  // more tiles than one launch takes: in parts (each a call of its own)
+        const int64_t tiles_seg = (nstripes * (ess / 16) + kTileChunksHost - 1) / kTileChunksHost;
+        const int64_t per = sets_max_tiles(4) / tiles_seg;
+        if (per < 1) return EC_ERR_UNSUPPORTED;
+        if ((int64_t)nseg > per) {
+            for (size_t g0 = 0; g0 < nseg; g0 += (size_t)per) {
+                std::vector<SetSeg> part(segs.begin() + g0, segs.begin() + std::min(nseg, g0 + (size_t)per));
+                std::vector<uint32_t> pbad;
+                const int rc = sets_call(c, part, nstripes, s, bad ? &pbad : nullptr);
+                if (rc) return rc;
+                if (bad) bad->insert(bad->end(), pbad.begin(), pbad.end());
+            }
+            return EC_OK;
+        }
+    }
     std::vector<int> idx(nseg);
     for (size_t g = 0; g < nseg; g++) idx[g] = (int)g;
     std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return segs[x].nw < segs[y].nw; });
@@ -1367,7 +1382,8 @@ void ec_destroy(ec_ctx *c) {
     {
         bool busy = false;
         std::lock_guard<std::mutex> g(c->sets.mu);
-        for (auto &x : c->sets.slots) busy = busy || (!x->dead && __atomic_load_n(x->h_words, __ATOMIC_ACQUIRE) != x->seq);
+        for (auto &x : c->sets.slots)  // (a dead slot's launches before the failed one may still run)
+            busy = busy || x->dead || __atomic_load_n(x->h_words, __ATOMIC_ACQUIRE) != x->seq;
         if (busy) (void)hipDeviceSynchronize();
         c->sets.slots.clear();
     }

@@ -511,7 +511,8 @@ hipError_t launch_matmul(const RsArgs &a, int grid, hipStream_t s) {
     // (rebuild of 16 RS(29,80) segments 419 -> 398 us, m = 29 28.1 -> 24.8 us
     // per segment).  The encoder keeps its persistent grid (one
     // workgroup per tile: 809 -> 1248 us).
-    if (grid <= 0) grid = (int)std::min<int64_t>(std::max<int64_t>(a.total_tiles, 1), 1 << 30);
+    // (the kernels loop over tiles past the grid; grid x workgroup size stays below 2^32 work-items)
+    if (grid <= 0) grid = (int)std::min<int64_t>(std::max<int64_t>(a.total_tiles, 1), 1 << 22);
     if (a.nout == 0 && !a.zero_check) {
         constexpr size_t kCopyLds = 58 * 1024;  // an occupancy cap: 2 workgroups per CU
         hipLaunchKernelGGL(rs_copy_shares<2>, dim3(grid), dim3(2 * 64), kCopyLds, s, a);

@@ -296,6 +296,8 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
 
 int sets_waves(int rows) { return rows <= 16 ? 2 : rows <= 24 ? 3 : 4; }
 
+int64_t sets_max_tiles(int nw) { return (int64_t)(0xFFFFFFFFu / (unsigned)(nw * 64)); }
+
 size_t sets_tgt_entries(int nin, int rows, int nw) {
     const int npass = rows > 0 ? (rows + nw * kRows - 1) / (nw * kRows) : 1;
     return (size_t)npass * nin * nw * kRows;
@@ -310,7 +312,7 @@ hipError_t launch_sets_prep(const SetStage *stage, SetDesc *desc, int nseg, uint
 
 hipError_t launch_matmul_sets(const SetsArgs &a, int nw, hipStream_t s) {
     if (a.total_tiles <= 0) return hipSuccess;
-    if (a.total_tiles > (int64_t)1 << 31) return hipErrorInvalidValue;
+    if (a.total_tiles > sets_max_tiles(nw)) return hipErrorInvalidValue;  // one workgroup per tile
     const dim3 grid((unsigned)a.total_tiles);
     switch (nw) {
     case 2: hipLaunchKernelGGL(rs_matmul_sets<2>, grid, dim3(2 * 64), (size_t)2 * 4 * 2048, s, a); break;

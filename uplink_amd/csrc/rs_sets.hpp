@@ -62,6 +62,9 @@ constexpr int64_t kTileChunksHost = 128;  // 16-byte chunks per tile (rs_tile.hp
 // rs_kernels.hip jt_waves: <= 16 -> 2, <= 24 -> 3, else 4, 8 rows per wave)
 int sets_waves(int rows);
 size_t sets_tgt_entries(int nin, int rows, int nw);  // 64-bit words of one segment's leaf table on nw waves
+// most tiles one rs_matmul_sets launch on nw waves takes (one workgroup per tile, the grid's
+// work-items below 2^32)
+int64_t sets_max_tiles(int nw);
 // one workgroup per segment; jt_base = address of leaf 0 (jt_table_base_addr);
 // zeroes *done_ctr for the launches that follow
 hipError_t launch_sets_prep(const SetStage *stage, SetDesc *desc, int nseg, uint64_t jt_base, uint32_t *done_ctr,
