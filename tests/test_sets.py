@@ -246,3 +246,46 @@ def test_batched_rebuild_fresh_sets_no_host_wait(oracle):
             assert np.array_equal(out.cpu().numpy(), seg)
     finally:
         c.close()
+
+
+def test_segment_codec_sets_host_mirror(oracle):
+    """The host mirror's SegmentCodec.rebuild_segments_sets /
+    decode_segments_sets (eestream.py) over the same exports: segments from
+    share sets of their own, one of them with a corrupted piece for Decode,
+    the errors Rebuild reports raised as the mirror's exceptions."""
+    from uplink_amd import eestream as E
+
+    k, n, ess, stripes, nseg = 20, 60, 256, 33, 6
+    rng = np.random.default_rng(2060)
+    segs = [rng.integers(0, 256, stripes * k * ess, dtype=np.uint8) for _ in range(nseg)]
+    f = oracle.FEC(k, n)
+    refs = np.stack([f.encode_segment(s, ess, threads=8) for s in segs])
+    scheme = E.new_rs_scheme(E.new_fec(k, n), ess)
+    codec = E.SegmentCodec(scheme)
+    try:
+        d_pieces = torch.from_numpy(refs.copy()).cuda()
+        plen = stripes * ess
+        sets = random_sets(rng, k, n, nseg, extra=3)
+        args = [(st, [d_pieces[g].data_ptr() + x * plen for x in st]) for g, st in enumerate(sets)]
+        outs = torch.zeros((nseg, stripes * k * ess), dtype=torch.uint8, device="cuda")
+        codec.rebuild_segments_sets(args, stripes, [outs[g] for g in range(nseg)])
+        torch.cuda.synchronize()
+        got = outs.cpu().numpy()
+        assert all(np.array_equal(got[g], segs[g]) for g in range(nseg))
+        bad = sets[2][1]
+        recv = refs.copy()
+        recv[2][bad] ^= 0x77
+        d2 = torch.from_numpy(recv).cuda()
+        args2 = [(st, [d2[g].data_ptr() + x * plen for x in st]) for g, st in enumerate(sets)]
+        outs.zero_()
+        codec.decode_segments_sets(args2, stripes, [outs[g] for g in range(nseg)])
+        got = outs.cpu().numpy()
+        assert all(np.array_equal(got[g], segs[g]) for g in range(nseg))
+        assert np.array_equal(d2.cpu().numpy(), refs)
+        with pytest.raises(E.NotEnoughShares):
+            codec.rebuild_segments_sets([(sets[0][:k - 1], args[0][1][:k - 1])], stripes, [outs[0]])
+        with pytest.raises(ValueError):
+            codec.rebuild_segments_sets(args, stripes, [outs[0]])
+    finally:
+        torch.cuda.synchronize()
+        scheme.close()

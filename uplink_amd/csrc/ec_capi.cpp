@@ -2725,10 +2725,16 @@ static int syndrome_plan(ec_ctx *c, const std::vector<int> &nums, PlanPtr *out) 
 
 // Fused Decode plan over the sorted share set (nums, all nshares of them as
 // inputs): first the rows of Rebuild -- the data shares infectious' share
-// choice leaves missing, from the shares it chooses (choose_shares) -- then the
-// syndrome rows of syndrome_plan.  One launch reads every share once, stores
-// the rebuilt rows (the present data shares are copied through) and checks
-// the syndrome rows for zero; *nrebuild = the number of rebuilt rows.
+// choice leaves missing, from the shares it chooses (choose_shares) -- then one
+// syndrome row per share it does not choose: that share minus its value
+// interpolated through the chosen ones.  One launch reads every share once,
+// stores the rebuilt rows (the present data shares are copied through) and
+// checks the syndrome rows for zero; *nrebuild = the number of rebuilt rows.
+// (Whether every share agrees with one codeword does not depend on which k
+// shares the syndromes are taken against; against the chosen ones, only those
+// k columns carry general coefficients -- every other column a single 1 -- so
+// each wave builds the 4-plane combinations of k inputs, not of the union of
+// two bases: Decode at k+20 (~11 more such inputs) 42.5 -> see DESIGN.md §4e.)
 static int fused_decode_plan(ec_ctx *c, const std::vector<int> &nums, PlanPtr *out, std::vector<int> &missing_out) {
     const int k = c->k, ns = (int)nums.size(), extra = ns - k;
     std::vector<int> order, ids;
@@ -2747,22 +2753,23 @@ static int fused_decode_plan(ec_ctx *c, const std::vector<int> &nums, PlanPtr *o
         for (int i = 0; i < k; i++)
             if (ids[i] >= k) missing.push_back(i);
         const int nreb = (int)missing.size();
-        // syndrome rows over the first k sorted shares
-        std::vector<uint8_t> b((size_t)k * k);
-        for (int i = 0; i < k; i++) memcpy(&b[(size_t)i * k], &c->G[(size_t)nums[i] * k], k);
-        if (!gf_invert(b.data(), k)) return EC_ERR_SINGULAR;
         rows = nreb + extra;
         M.assign((size_t)std::max(rows, 1) * ns, 0);
         for (int r = 0; r < nreb; r++)
             for (int i = 0; i < k; i++) M[(size_t)r * ns + order[i]] = m[(size_t)missing[r] * k + i];
-        for (int r = 0; r < extra; r++) {
-            uint8_t *row = &M[(size_t)(nreb + r) * ns];
-            for (int col = 0; col < k; col++) {
+        // syndrome rows: share u (not chosen) minus G_u (G_chosen)^-1 applied to the chosen shares
+        std::vector<char> chosen(ns, 0);
+        for (int i = 0; i < k; i++) chosen[order[i]] = 1;
+        int r = nreb;
+        for (int u = 0; u < ns; u++) {
+            if (chosen[u]) continue;
+            uint8_t *row = &M[(size_t)r++ * ns];
+            for (int i = 0; i < k; i++) {
                 uint8_t acc = 0;
-                for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[k + r] * k + t], b[(size_t)t * k + col]);
-                row[col] = acc;
+                for (int t = 0; t < k; t++) acc ^= gf_mul(c->G[(size_t)nums[u] * k + t], m[(size_t)t * k + i]);
+                row[order[i]] = acc;
             }
-            row[k + r] = 1;
+            row[u] = 1;
         }
         return EC_OK;
     }, out, ns);

@@ -441,6 +441,10 @@ class SegmentCodec:
     rebuild_segments(nums, piece_ptrs, nstripes, out, nseg=1, piece_seg_stride=0,
                      out_seg_stride=0, stream=None)
         out    [nseg][nstripes][k][ess]
+    rebuild_segments_sets(sets, nstripes, outs, stream=None)
+    decode_segments_sets(sets, nstripes, outs, stream=None)
+        sets   one (nums, piece_ptrs) per segment: each segment with its own share set
+        outs   one [nstripes][k][ess] output per segment
     """
 
     def __init__(self, scheme: RSScheme):
@@ -494,4 +498,40 @@ class SegmentCodec:
         rc = self._lib.ec_rebuild_segments_batched(self.scheme.ctx, len(nums), c_nums, c_ptrs, nstripes, nseg,
                                                    piece_seg_stride, out_seg_stride, self._addr(out),
                                                    self._stream(stream))
+        _raise(self.scheme.ctx, rc)
+
+    def _sets_args(self, sets, outs):
+        sets = [(list(nums), [self._addr(p) for p in ptrs]) for nums, ptrs in sets]
+        outs = [self._addr(o) for o in outs]
+        if len(outs) != len(sets):
+            raise ValueError("one output per segment")
+        for nums, ptrs in sets:
+            if len(nums) != len(ptrs):
+                raise ValueError("nums and piece pointers differ in length")
+        nseg = len(sets)
+        flat_n = [x for nums, _ in sets for x in nums]
+        flat_p = [x for _, ptrs in sets for x in ptrs]
+        return (nseg, (ctypes.c_int * max(nseg, 1))(*[len(nums) for nums, _ in sets]),
+                (ctypes.c_int * max(len(flat_n), 1))(*flat_n), (ctypes.c_void_p * max(len(flat_p), 1))(*flat_p),
+                (ctypes.c_void_p * max(nseg, 1))(*outs))
+
+    def rebuild_segments_sets(self, sets, nstripes: int, outs, stream=None):
+        """Rebuild of many segments, each from a share set of its own, in one
+        stream-ordered pass (ec_rebuild_segments_sets): what one StripeReader
+        per download does for each segment with whichever k pieces answered
+        first (stripe.go:314-354, client.go:273-308), several segments at once
+        under prefetch (store.go:240-253).  Asynchronous on `stream`."""
+        nseg, nsh, nums, ptrs, optr = self._sets_args(sets, outs)
+        rc = self._lib.ec_rebuild_segments_sets(self.scheme.ctx, nseg, nsh, nums, ptrs, nstripes, optr,
+                                                self._stream(stream))
+        _raise(self.scheme.ctx, rc)
+
+    def decode_segments_sets(self, sets, nstripes: int, outs, stream=None):
+        """Decode (Correct + Rebuild) of many segments, a share set each
+        (ec_decode_segments_sets); a segment with errors has its pieces
+        corrected in place, as infectious corrects share.Data; returns when
+        done."""
+        nseg, nsh, nums, ptrs, optr = self._sets_args(sets, outs)
+        rc = self._lib.ec_decode_segments_sets(self.scheme.ctx, nseg, nsh, nums, ptrs, nstripes, optr,
+                                               self._stream(stream))
         _raise(self.scheme.ctx, rc)
