@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample-s", type=float, default=5.0)
+    ap.add_argument("--lib", default=None, help="another build of the library (A/B)")
     args = ap.parse_args()
+    if args.lib:
+        from uplink_amd import _native
+        _native.load(args.lib)  # (the process's library from here on)
     torch.cuda.set_device(0)
     nseg = args.nseg
     rng = np.random.default_rng(3)

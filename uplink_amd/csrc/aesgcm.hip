@@ -23,8 +23,11 @@
 // (leading zero slots do not change it).  Lanes whose first slot is padding
 // compute AES(K, J0) instead, which masks the tag.
 //
-// AES: T-tables in LDS, round keys in SGPRs.  GHASH: Shoup's 4-bit tables of
-// H^1..H^64 in LDS (16 KB per key, built on the host by gcm_prepare).
+// AES: T-tables in LDS, round keys in SGPRs.  GHASH: the Horner steps on an
+// 8-bit table of H^64 (16 lookups per product), the final products by
+// H^(64-l) on Shoup's 4-bit tables of H^1..H^64, all in LDS (20 KB per key,
+// built on the host by gcm_prepare).  36.6 KB of LDS and 128 VGPRs per
+// workgroup of 4 waves: four workgroups per CU.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -87,16 +90,39 @@ __device__ constexpr uint32_t kRem4[16] = {0x0000u << 16, 0x1C20u << 16, 0x3840u
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
 
+// Reduction constants for an 8-bit shift (the bits of the shifted-out byte
+// folded back through x^128 = x^7 + x^2 + x + 1, reflected): the top 16 bits of word 0
+struct Rem8 {
+    uint16_t r[256];
+    constexpr Rem8() : r{} {
+        for (int b = 0; b < 256; b++) {
+            uint64_t hi = 0, lo = (uint64_t)b;
+            for (int i = 0; i < 8; i++) {
+                const uint64_t carry = lo & 1;
+                lo = (lo >> 1) | (hi << 63);
+                hi = (hi >> 1) ^ (carry ? 0xE100000000000000ull : 0);
+            }
+            r[b] = (uint16_t)(hi >> 48);
+        }
+    }
+};
+__device__ constexpr Rem8 kRem8{};
+
 // T-table layout: T0 alone, replicated kCopies times with copy c of entry x
-// at word x*kCopies + c; lane l reads copy l % kCopies, so at most two lanes
-// share an LDS bank; T1..T3 are rotations of T0 (DESIGN.md §4c has the
-// measured alternatives).
-constexpr int kCopies = 32;
+// at word x*kCopies + c; lane l reads copy l % kCopies; T1..T3 are rotations
+// of T0.  16 copies (16 KB) with four workgroups per CU beat 32 copies with
+// three (DESIGN.md §4c has the measured alternatives).
+#ifndef UPLINK_GCM_COPIES  // (-D for A/B builds)
+#define UPLINK_GCM_COPIES 16
+#endif
+constexpr int kCopies = UPLINK_GCM_COPIES;
 
 struct Lds {
     uint32_t t[256 * kCopies];
     uint32_t rem[16];
     uint32_t htab[64][16][4];    // H^1..H^64
+    uint32_t h8[256][4];         // byte * H^64
+    uint16_t rem8[256];          // (16 bits each: with three workgroups' tables the CU's LDS is full)
 };
 
 // Tk[x] for this lane
@@ -152,14 +178,39 @@ __device__ __forceinline__ void gf_mul(uint32_t (&z)[4], const uint32_t (&x)[4],
     z[0] = z0, z[1] = z1, z[2] = z2, z[3] = z3;
 }
 
+// z = x * E with E's 8-bit table (one lookup and one reduction per byte: half
+// the steps of gf_mul's 4-bit table)
+__device__ __forceinline__ void gf_mul8(uint32_t (&z)[4], const uint32_t (&x)[4], const uint32_t (*tab)[4],
+                                        const uint16_t *rem8) {
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+    for (int i = 15; i >= 0; i--) {
+        const uint32_t byte = (x[i >> 2] >> ((3 - (i & 3)) * 8)) & 0xff;
+        if (i != 15) {
+            const uint32_t r = (uint32_t)rem8[z3 & 0xff] << 16;
+            z3 = __builtin_amdgcn_alignbit(z2, z3, 8);
+            z2 = __builtin_amdgcn_alignbit(z1, z2, 8);
+            z1 = __builtin_amdgcn_alignbit(z0, z1, 8);
+            z0 = (z0 >> 8) ^ r;
+        }
+        const uint4 t = *reinterpret_cast<const uint4 *>(tab[byte]);
+        z0 ^= t.x, z1 ^= t.y, z2 ^= t.z, z3 ^= t.w;
+    }
+    z[0] = z0, z[1] = z1, z[2] = z2, z[3] = z3;
+}
+
 // bytes [0, n) of the 16-byte word at p (n < 16), big-endian words, zero padded
 __device__ __forceinline__ void load_tail(const uint8_t *p, uint32_t n, uint32_t (&w)[4]) {
     w[0] = w[1] = w[2] = w[3] = 0;
     for (uint32_t i = 0; i < n; i++) w[i >> 2] |= (uint32_t)p[i] << (24 - 8 * (i & 3));
 }
 
+#ifndef UPLINK_GCM_WAVES_PER_EU  // (-D for A/B builds: a register budget of 512 / this per lane)
+#define UPLINK_GCM_WAVES_PER_EU 4
+#endif
 template <bool kOpen>
-__global__ __launch_bounds__(256, 1) void gcm_blocks(GcmBatch a, uint32_t wgs_per_seg) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UPLINK_GCM_WAVES_PER_EU))) void gcm_blocks(
+    GcmBatch a, uint32_t wgs_per_seg) {
     __shared__ Lds L;
     const uint32_t seg = blockIdx.x / wgs_per_seg;
     const uint32_t wg = blockIdx.x % wgs_per_seg;
@@ -170,6 +221,12 @@ __global__ __launch_bounds__(256, 1) void gcm_blocks(GcmBatch a, uint32_t wgs_pe
         const uint4 *src = reinterpret_cast<const uint4 *>(&ks->htab[0][0][0]);
         uint4 *dst = reinterpret_cast<uint4 *>(&L.htab[0][0][0]);
         for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) dst[i] = src[i];
+        const uint4 *s8 = reinterpret_cast<const uint4 *>(&ks->h64_8[0][0]);
+        uint4 *d8 = reinterpret_cast<uint4 *>(&L.h8[0][0]);
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+            d8[i] = s8[i];
+            L.rem8[i] = kRem8.r[i];
+        }
     }
     __syncthreads();
     uint32_t rk[60];
@@ -251,7 +308,7 @@ __global__ __launch_bounds__(256, 1) void gcm_blocks(GcmBatch a, uint32_t wgs_pe
             // Horner step with H^64
             if (j) {
                 uint32_t m[4];
-                gf_mul(m, acc, L.htab[63], L.rem);
+                gf_mul8(m, acc, L.h8, L.rem8);
 #pragma unroll
                 for (int q = 0; q < 4; q++) acc[q] = m[q] ^ y[q];
             } else {
@@ -332,6 +389,25 @@ U128 gf_mul_bits(U128 x, U128 y) {  // GCM spec Algorithm 1
     return z;
 }
 
+// tab[b] = b * e for every byte b (bit 7 of b the coefficient of x^0)
+void shoup_table8(U128 e, uint32_t tab[256][4]) {
+    U128 t[256] = {};
+    t[128] = e;
+    U128 v = e;
+    for (int i = 64; i > 0; i >>= 1) {
+        const uint64_t carry = v.lo & 1;
+        v.lo = (v.lo >> 1) | (v.hi << 63);
+        v.hi = (v.hi >> 1) ^ (carry ? 0xE100000000000000ull : 0);
+        t[i] = v;
+    }
+    for (int i = 2; i < 256; i <<= 1)
+        for (int j = 1; j < i; j++) t[i + j] = U128{t[i].hi ^ t[j].hi, t[i].lo ^ t[j].lo};
+    for (int i = 0; i < 256; i++) {
+        tab[i][0] = (uint32_t)(t[i].hi >> 32), tab[i][1] = (uint32_t)t[i].hi;
+        tab[i][2] = (uint32_t)(t[i].lo >> 32), tab[i][3] = (uint32_t)t[i].lo;
+    }
+}
+
 void shoup_table(U128 e, uint32_t tab[16][4]) {
     U128 t[16] = {};
     t[8] = e;
@@ -387,6 +463,7 @@ void gcm_prepare(const uint8_t key[32], GcmSched *out) {
     U128 p = H;
     for (int k = 0; k < 64; k++) {  // htab[k] = table of H^(k+1)
         shoup_table(p, out->htab[k]);
+        if (k == 63) shoup_table8(p, out->h64_8);
         p = gf_mul_bits(p, H);
     }
 }

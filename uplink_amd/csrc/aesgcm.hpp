@@ -14,6 +14,7 @@ struct GcmSched {
     uint32_t rk[60];
     uint32_t pad_[4];
     uint32_t htab[64][16][4];  // htab[p][nibble] = nibble * H^(p+1) (Shoup's 4-bit table)
+    uint32_t h64_8[256][4];    // byte * H^64 (the 8-bit table of the Horner multiplier)
 };
 
 // Fills `out` with the schedule of a 32-byte key (host memory).
