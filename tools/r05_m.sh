@@ -4,7 +4,7 @@
 # rocprofv3 --kernel-trace --stats.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${1:-r05/m}
+O=gpurun_out/${1:-r05/m2}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_aesgcm.py tests/test_pipeline.py -m gpu > $O/pytest.log 2>&1
 timeout -k 10 200 python -u tools/bench_gcm.py > $O/bench_gcm.json 2> $O/bench_gcm.err

@@ -30,6 +30,7 @@
 // workgroup of 4 waves: four workgroups per CU.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -471,9 +472,16 @@ void gcm_prepare(const uint8_t key[32], GcmSched *out) {
 hipError_t gcm_launch(const GcmBatch &b, bool open, hipStream_t stream) {
     if (b.nseg == 0 || b.nblocks == 0) return hipSuccess;
     if (b.in_block == 0 || b.in_block > (1u << 24)) return hipErrorInvalidValue;
-    // enough workgroups to fill the chip several times, each looping over blocks of one segment
+    // enough workgroups to fill the chip many times over, each looping over blocks of one segment:
+    // 32 per CU (8 segments: seal 167.3 us per segment, against 168.3 at 16, 174.7 at 8, 184.0 at
+    // 4; profiles/r05/gcm/ab_grid*.json; UPLINK_GCM_GRID_PER_CU for A/B)
+    static const uint64_t per_cu = [] {
+        const char *e = getenv("UPLINK_GCM_GRID_PER_CU");
+        const int v = e ? atoi(e) : 32;
+        return (uint64_t)(v > 0 && v <= 64 ? v : 32);
+    }();
     uint32_t wgs = (b.nblocks + 3) / 4;
-    const uint32_t cap = (uint32_t)((256ull * 8 + b.nseg - 1) / b.nseg);
+    const uint32_t cap = (uint32_t)((256ull * per_cu + b.nseg - 1) / b.nseg);
     if (wgs > cap) wgs = cap < 1 ? 1 : cap;
     const dim3 grid(b.nseg * wgs);
     if (open)
