@@ -289,3 +289,43 @@ def test_segment_codec_sets_host_mirror(oracle):
     finally:
         torch.cuda.synchronize()
         scheme.close()
+
+
+@pytest.mark.parametrize("decode", [False, True])
+def test_sets_segments_off_the_bit_sliced_path(oracle, decode):
+    """Segments the share-set pass cannot take go through the single-set paths
+    inside the same call, with the same results: a share size that is not a
+    multiple of 16 (the byte kernel), and, at ess 256, one segment whose
+    output and one whose piece is not 16-byte aligned, beside aligned ones."""
+    rng = np.random.default_rng(100 + decode)
+    for k, n, ess, stripes in [(4, 10, 100, 37), (29, 80, 256, 9)]:
+        nseg = 4
+        segs = [rng.integers(0, 256, stripes * k * ess, dtype=np.uint8) for _ in range(nseg)]
+        plen = stripes * ess
+        f = oracle.FEC(k, n)
+        refs = np.stack([f.encode_segment(s, ess, threads=8) for s in segs])
+        # pieces and outputs in buffers 16 bytes longer, so a segment can sit 8 bytes in
+        d_pieces = torch.zeros((nseg, n * plen + 16), dtype=torch.uint8, device="cuda")
+        outs = torch.zeros((nseg, stripes * k * ess + 16), dtype=torch.uint8, device="cuda")
+        pshift = [0, 8, 0, 0] if ess % 16 == 0 else [0] * nseg
+        oshift = [0, 0, 8, 0] if ess % 16 == 0 else [0] * nseg
+        for g in range(nseg):
+            d_pieces[g, pshift[g]:pshift[g] + n * plen] = torch.from_numpy(refs[g].reshape(-1)).cuda()
+        sets = random_sets(rng, k, n, nseg, extra=2 if decode else 0)
+        c = Ctx(k, n, ess)
+        try:
+            nsh = (ctypes.c_int * nseg)(*[len(s) for s in sets])
+            flat = [x for s in sets for x in s]
+            nums = (ctypes.c_int * len(flat))(*flat)
+            ptrs = (ctypes.c_void_p * len(flat))(
+                *[d_pieces[g].data_ptr() + pshift[g] + x * plen for g, s in enumerate(sets) for x in s])
+            optr = (ctypes.c_void_p * nseg)(*[outs[g].data_ptr() + oshift[g] for g in range(nseg)])
+            fn = c.L.ec_decode_segments_sets if decode else c.L.ec_rebuild_segments_sets
+            rc = fn(c.ctx, nseg, nsh, nums, ptrs, stripes, optr, torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, _native.strerror(rc)
+            torch.cuda.synchronize()
+            got = outs.cpu().numpy()
+            for g in range(nseg):
+                assert np.array_equal(got[g, oshift[g]:oshift[g] + stripes * k * ess], segs[g]), (k, ess, g)
+        finally:
+            c.close()
