@@ -294,7 +294,11 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
 
 }  // namespace
 
-int sets_waves(int rows) { return rows <= 16 ? 2 : rows <= 24 ? 3 : 4; }
+// as the straight-line split (rs_sl_codegen.cpp split_for): 15-16 rows on 3 waves, not 2 -- one
+// share set of 15 rows, 32 segments: 794-848 against 821-866 us on 2 waves, 815-834 on 4
+// (profiles/r05/r/); the 14-24-row mix of fresh sets on 4 waves instead of 3: 874-882 against
+// 855-857 us, one segment 73.5 against 62-64 us wall (profiles/r05/q/)
+int sets_waves(int rows) { return rows <= 14 ? 2 : rows <= 24 ? 3 : 4; }
 
 int64_t sets_max_tiles(int nw) { return (int64_t)(0xFFFFFFFFu / (unsigned)(nw * 64)); }
 

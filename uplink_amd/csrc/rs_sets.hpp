@@ -58,8 +58,8 @@ struct SetsArgs {
 
 constexpr int64_t kTileChunksHost = 128;  // 16-byte chunks per tile (rs_tile.hpp kTileChunks)
 
-// waves per workgroup for `rows` computed rows (the jump-table body's split,
-// rs_kernels.hip jt_waves: <= 16 -> 2, <= 24 -> 3, else 4, 8 rows per wave)
+// waves per workgroup for `rows` computed rows (<= 14 -> 2, <= 24 -> 3, else 4,
+// at most 8 rows per wave)
 int sets_waves(int rows);
 size_t sets_tgt_entries(int nin, int rows, int nw);  // 64-bit words of one segment's leaf table on nw waves
 // most tiles one rs_matmul_sets launch on nw waves takes (one workgroup per tile, the grid's
