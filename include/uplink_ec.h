@@ -345,6 +345,11 @@ int ec_set_body(ec_ctx *ctx, int body);
 /* which body the ctx's last runtime-matrix launch used: EC_BODY_JUMP_TABLE,
  * EC_BODY_STRAIGHT_LINE, or EC_BODY_AUTO when there was none yet */
 int ec_last_body(const ec_ctx *ctx);
+/* Compile-time encoder launches of this ctx so far that took a work-counter
+ * slot (tiles handed out by a queue) and that assigned their tiles statically
+ * because no slot was free without waiting for another stream (identical
+ * results; a diagnostic).  No reference counterpart. */
+int ec_encoder_queue_stats(const ec_ctx *ctx, unsigned long long *queued, unsigned long long *static_tiles);
 /* Identity of this build: 16 hex digits of a SHA-256 over the library's
  * sources, generators and build flags (uplink_amd/csrc/Makefile).  Measurement
  * records taken from one build (profiles/pmc_traffic.json) carry it, so a bench

@@ -1050,6 +1050,38 @@ def test_encoder_queue_reused_across_streams(oracle):
         L.ec_destroy(ctx)
 
 
+def test_encoder_queue_survives_many_short_lived_streams(oracle):
+    """A stream that encodes a few times and goes away (a stream per request)
+    does not keep a work-counter slot from the others: 48 streams,
+    more than the 32 slots, each encoding twice and then dropped; later
+    launches still take a slot (ec_encoder_queue_stats), and every result
+    matches the oracle."""
+    k, n, ess, stripes = 29, 80, 256, 96
+    L = _native.load()
+    ctx = ctypes.c_void_p()
+    assert L.ec_create(k, n, ess, ctypes.byref(ctx)) == 0
+    rng = np.random.default_rng(48)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess)
+    d_seg = torch.from_numpy(seg).cuda()
+    try:
+        for i in range(48):
+            st = torch.cuda.Stream()
+            for _ in range(2):
+                d = torch.empty((n, stripes * ess), dtype=torch.uint8, device="cuda")
+                assert L.ec_encode_segments(ctx, d_seg.data_ptr(), 1, stripes, d.data_ptr(), 0, st.cuda_stream) == 0
+                st.synchronize()
+                assert np.array_equal(d.cpu().numpy(), ref), i
+            del st
+        q, s = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        assert L.ec_encoder_queue_stats(ctx, ctypes.byref(q), ctypes.byref(s)) == 0
+        assert q.value + s.value == 96
+        assert s.value == 0, (q.value, s.value)  # every launch found a slot
+    finally:
+        torch.cuda.synchronize()
+        L.ec_destroy(ctx)
+
+
 @pytest.mark.parametrize("body", ["jt", "sl"])
 def test_decode_segments_fused_pass_every_shape(oracle, body):
     """The fused Decode launch: rebuilt data rows stored,

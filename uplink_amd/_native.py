@@ -110,6 +110,8 @@ SIGNATURES = {
     "ec_prepare_encoder": (ctypes.c_int, [vp, ctypes.c_int]),
     "ec_set_body": (ctypes.c_int, [vp, ctypes.c_int]),
     "ec_last_body": (ctypes.c_int, [vp]),
+    "ec_encoder_queue_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_ulonglong),
+                                              ctypes.POINTER(ctypes.c_ulonglong)]),
     "ec_build_id": (ctypes.c_char_p, []),
 }
 

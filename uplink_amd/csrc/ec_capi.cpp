@@ -340,30 +340,31 @@ struct SlBuilder {
 // Work counters of the compile-time encoder's launches (RsArgs::queue): a
 // ring of counter pairs (tile counter, workgroups done), zeroed once when the
 // ring is made.  The last workgroup of a launch puts its pair back to zero
-// (rs_encoder.hpp), so a launch needs no memset before it.  A slot serves one
-// launch at a time: it goes to a launch on the stream its previous launch ran
-// on (stream order), or to another stream once an event recorded right behind
-// its previous launch has completed; with no such slot the launch assigns its
-// tiles statically (identical results).  No launch waits on another stream.
-// The event is recorded behind every kEventEvery-th launch of a slot only (a
-// marker on the stream costs a few microseconds per launch): a slot whose
-// latest launch has none is reused by its own stream alone.
+// (rs_encoder.hpp), so a launch needs no memset before it, and then stores the
+// launch's sequence number into the slot's completion word in pinned host
+// memory.  A slot serves one launch at a time: it goes to a launch on the
+// stream its previous launch ran on (stream order), or to any stream once its
+// completion word shows that its latest launch has finished; with no such
+// slot the launch assigns its tiles statically (identical results).  No launch
+// waits on another stream and none needs an event or marker on its stream, so
+// a stream that launches a few times and goes away leaves its slot to the
+// others.
 struct QueueRing {
     static constexpr int kSlots = 32;
     static constexpr int kStride = 64;  // words per slot: the counter pair (kQueueDoneWord), a slot per 256 bytes
     std::mutex mu;
     uint32_t *d = nullptr;
-    int event_every = 8;                // UPLINK_EC_QUEUE_EVENT_EVERY at ec_create (A/B measurements)
-    hipEvent_t ev[kSlots] = {};
+    uint32_t *h_done = nullptr;         // pinned, coherent: [slot] sequence number of its latest finished launch
+    uint32_t seq[kSlots] = {};          // [slot] sequence number of its latest launch
     hipStream_t owner[kSlots] = {};     // stream of the slot's last launch
     bool used[kSlots] = {}, busy[kSlots] = {};
-    bool covered[kSlots] = {};          // the event follows the slot's latest launch
-    int since[kSlots] = {};             // the slot's launches since its last event
+    bool done(int i) const { return __atomic_load_n(h_done + i, __ATOMIC_ACQUIRE) == seq[i]; }
 };
 
 struct ec_ctx {
     int k = 0, n = 0, ess = 0, device = 0;
     QueueRing qring;
+    std::atomic<uint64_t> q_taken{0}, q_static{0};  // encoder launches with a counter slot / static tiles
     std::mutex pipe_mu;  // one host pipeline at a time per context
     HostPipe pipe;
     std::mutex upload_mu;
@@ -673,12 +674,13 @@ int after_launch(uint32_t *chk, hipStream_t s) {
     return EC_OK;
 }
 
-// A zeroed work counter for one encoder launch on stream s (slot in *slot;
+// A zeroed work counter for one encoder launch on stream s (slot in *slot, the
+// launch's sequence number in *seq and the slot's completion word in *done;
 // queue_done after the launch).  nullptr when none can be had without waiting
 // for another stream: the kernel then assigns its tiles statically, with
 // identical results.  (A stream handle is taken to name one stream while work
 // queued on it is in flight.)
-uint32_t *queue_take(ec_ctx *c, hipStream_t s, int *slot) {
+uint32_t *queue_take(ec_ctx *c, hipStream_t s, int *slot, uint32_t *seq, uint32_t **done) {
     QueueRing &q = c->qring;
     std::lock_guard<std::mutex> g(q.mu);
     if (!q.d) {
@@ -687,42 +689,43 @@ uint32_t *queue_take(ec_ctx *c, hipStream_t s, int *slot) {
             q.d = nullptr;
             return nullptr;
         }
-        if (hipMemset(q.d, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        if (hipHostMalloc((void **)&q.h_done, sizeof(uint32_t) * QueueRing::kSlots,
+                          hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+            q.h_done = nullptr;
             (void)hipFree(q.d);
             q.d = nullptr;
             return nullptr;
         }
-        for (int i = 0; i < QueueRing::kSlots; i++)
-            if (hipEventCreateWithFlags(&q.ev[i], hipEventDisableTiming) != hipSuccess) q.ev[i] = nullptr;
+        memset(q.h_done, 0, sizeof(uint32_t) * QueueRing::kSlots);
+        if (hipMemset(q.d, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipHostFree(q.h_done);
+            (void)hipFree(q.d);
+            q.d = nullptr, q.h_done = nullptr;
+            return nullptr;
+        }
     }
     int pick = -1;
     // the slot this stream used last: its previous launch precedes this one in stream order
     for (int i = 0; i < QueueRing::kSlots && pick < 0; i++)
-        if (q.used[i] && !q.busy[i] && q.owner[i] == s && q.ev[i]) pick = i;
-    // else a fresh slot, or one whose last launch (on another stream) has completed
+        if (q.used[i] && !q.busy[i] && q.owner[i] == s) pick = i;
+    // else a fresh slot, or one whose latest launch (on any stream) has finished
     for (int i = 0; i < QueueRing::kSlots && pick < 0; i++)
-        if (!q.busy[i] && q.ev[i] && (!q.used[i] || (q.covered[i] && hipEventQuery(q.ev[i]) == hipSuccess))) pick = i;
+        if (!q.busy[i] && (!q.used[i] || q.done(i))) pick = i;
     if (pick < 0) return nullptr;
     q.busy[pick] = true;
     *slot = pick;
+    *seq = q.seq[pick] + 1;
+    *done = q.h_done + pick;
     return q.d + (size_t)pick * QueueRing::kStride;
 }
 
-void queue_done(ec_ctx *c, hipStream_t s, int slot, bool launched) {
+void queue_done(ec_ctx *c, hipStream_t s, int slot, uint32_t seq, bool launched) {
     QueueRing &q = c->qring;
     std::lock_guard<std::mutex> g(q.mu);
     if (launched) {
-        // a slot's first launch for a stream that did not own it gets its event at once, so a
-        // stream that launches a few times and goes away (a stream per request) does not keep
-        // the slot from every other stream for good
-        const bool new_owner = !q.used[slot] || q.owner[slot] != s;
         q.used[slot] = true;
         q.owner[slot] = s;
-        q.covered[slot] = false;
-        if (new_owner || ++q.since[slot] >= q.event_every) {
-            q.since[slot] = 0;
-            q.covered[slot] = hipEventRecord(q.ev[slot], s) == hipSuccess;
-        }
+        q.seq[slot] = seq;
     }
     q.busy[slot] = false;
 }
@@ -1314,6 +1317,13 @@ int ec_set_body(ec_ctx *c, int body) {
 
 int ec_last_body(const ec_ctx *c) { return c ? c->last_body : EC_BODY_AUTO; }
 
+int ec_encoder_queue_stats(const ec_ctx *c, unsigned long long *queued, unsigned long long *static_tiles) {
+    if (!c || !queued || !static_tiles) return EC_ERR_INVALID_ARG;
+    *queued = c->q_taken.load(std::memory_order_relaxed);
+    *static_tiles = c->q_static.load(std::memory_order_relaxed);
+    return EC_OK;
+}
+
 // UPLINK_EC_BUILD_ID: generated by the Makefile into the build directory
 // (build_id.inc) from a digest of the sources, generators and flags.
 const char *ec_build_id(void) {
@@ -1364,7 +1374,6 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
     HIP_TRY(hipMalloc(&c->d_chk, 4));
     HIP_TRY(hipMemset(c->d_chk, 0, 4));
 #endif
-    if (const char *e = getenv("UPLINK_EC_QUEUE_EVENT_EVERY")) c->qring.event_every = std::max(1, atoi(e));
     if (const char *e = getenv("UPLINK_EC_SETS_MERGE")) c->sets_merge = atoi(e) != 0;
     if (const char *e = getenv("UPLINK_EC_SETS_STAGE_DMA")) c->sets_stage_dma = atoi(e) != 0;
     configure_rebuild(getenv("UPLINK_EC_REBUILD_DEPTH") ? atoi(getenv("UPLINK_EC_REBUILD_DEPTH")) : 1);
@@ -1404,14 +1413,13 @@ void ec_destroy(ec_ctx *c) {
     c->enc_row.clear();
     if (c->setup) (void)hipStreamSynchronize(c->setup), (void)hipStreamDestroy(c->setup);
     if (c->d_chk) (void)hipFree(c->d_chk);
-    // a slot whose latest launch has no event behind it may still be in use on a
-    // caller's stream: then wait for the device before the counters are freed
-    bool uncovered = false;
-    for (int i = 0; i < QueueRing::kSlots; i++) uncovered = uncovered || (c->qring.used[i] && !c->qring.covered[i]);
-    if (uncovered) (void)hipDeviceSynchronize();
-    for (int i = 0; i < QueueRing::kSlots; i++)
-        if (c->qring.ev[i]) (void)hipEventSynchronize(c->qring.ev[i]), (void)hipEventDestroy(c->qring.ev[i]);
+    // a counter slot whose latest launch has not finished may still be in use on a caller's
+    // stream: then wait for the device before the counters are freed
+    bool pending = false;
+    for (int i = 0; i < QueueRing::kSlots && c->qring.h_done; i++) pending = pending || (c->qring.used[i] && !c->qring.done(i));
+    if (pending) (void)hipDeviceSynchronize();
     if (c->qring.d) (void)hipFree(c->qring.d);
+    if (c->qring.h_done) (void)hipHostFree(c->qring.h_done);
     delete c;
 }
 
@@ -1516,9 +1524,10 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
             a.coef = nullptr;
             set_extents(a, (int64_t)nseg, c->d_chk);
             int slot = -1;
-            a.queue = queue_take(c, s, &slot);
+            a.queue = queue_take(c, s, &slot, &a.queue_seq, &a.queue_host_done);
+            (a.queue ? c->q_taken : c->q_static).fetch_add(1, std::memory_order_relaxed);
             const hipError_t e = launch_encode_special(*ek, a, 0, s);
-            if (slot >= 0) queue_done(c, s, slot, e == hipSuccess);
+            if (slot >= 0) queue_done(c, s, slot, a.queue_seq, e == hipSuccess);
             HIP_TRY(e);
             return after_launch(c->d_chk, s);
         }

@@ -49,6 +49,8 @@ struct RsArgs {
     int64_t blocks_per_seg;   // ceil(chunks_per_seg / 64)
     int64_t total_blocks;     // blocks_per_seg * nseg
     uint32_t *queue;          // zero work counters of this launch, see kQueueDoneWord (null: static assignment)
+    uint32_t *queue_host_done;  // with queue: the slot's completion word (pinned host memory)
+    uint32_t queue_seq;       // stored there by the launch's last workgroup
     // runtime-matrix kernel: when set, the computed rows from nstore on are
     // checked for zero instead of stored (syndrome rows of ec_decode_segments);
     // each wave that finds a non-zero byte in a valid column adds 1 here

@@ -396,10 +396,14 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
     // that gets it (so none needs a memset before it).  Every take of this
     // workgroup has returned (its value was used above) before its done count
     // is added, so when the count reaches gridDim.x no take of the launch is left.
+    // Then it tells the host, through the slot's completion word, that the slot
+    // may go to a launch on another stream.
     if (taker && a.queue) {
         if (atomicAdd(a.queue + kQueueDoneWord, 1u) == gridDim.x - 1) {
             atomicExch(a.queue, 0u);
             atomicExch(a.queue + kQueueDoneWord, 0u);
+            if (a.queue_host_done)
+                __hip_atomic_store(a.queue_host_done, a.queue_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
