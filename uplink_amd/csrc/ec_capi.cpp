@@ -6,410 +6,17 @@
 // the decode matrix (once per share set, cached), and staging of
 // host buffers for the per-stripe ErasureScheme calls.  Every byte of share
 // data is produced by a GPU kernel.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <chrono>
-#include <condition_variable>
-#include <cstdio>
-#include <cstring>
-#include <list>
-#include <memory>
-#include <deque>
-#include <atomic>
-#include <mutex>
-#include <set>
-#include <thread>
-#include <vector>
-
-#include "../../include/uplink_ec.h"
-#include "blake3.hpp"
-#include "ec_log.hpp"
-#include "gf256.hpp"
-#include "rs_correct.hpp"
-#include "rs_kernels.hpp"
-#include "rs_sets.hpp"
-#include "rs_sl.hpp"
-
-using namespace uplink_ec;
-
-namespace {
-
-// A runtime matrix M (rows x nin) uploaded for the generic kernels: the
-// coefficients coef[j][r] = M[r][j] and, for the bit-sliced kernel, the
-// jump-table leaf addresses of every block of up to kMaxOps rows
-// (launch_jt_targets).  Plans are built once -- synchronously, on the
-// context's own setup stream -- and reused by every launch of that matrix, so
-// no launch allocates memory or prepares tables in stream order.
 //
-// Plans of at most kMaxOps rows can also carry the matrix as straight-line
-// code (rs_sl.hpp): a module made from the template code object on the first
-// launch that wants it, and the absolute addresses of its segments.
-// Device memory for the plans' small tables (coefficients, leaf addresses,
-// segment addresses), carved from 2-MiB chunks in power-of-two classes and
-// recycled, so that making or evicting a plan costs no hipMalloc / hipFree
-// (a fresh share set per segment is the download path's common case).  The
-// chunks go back to HIP when the context and every plan are gone.
-struct DevArena {
-    static constexpr size_t kChunk = 2u << 20, kMinClass = 256;
-    std::mutex mu;
-    std::vector<void *> chunks;
-    uint8_t *cur = nullptr;
-    size_t left = 0;
-    std::vector<std::vector<uint8_t *>> free_by_class = std::vector<std::vector<uint8_t *>>(32);
-    static int cls(size_t n) {
-        int c = 0;
-        while ((kMinClass << c) < n) c++;
-        return c;
-    }
-    uint8_t *alloc(size_t n) {
-        const int c = cls(n);
-        const size_t sz = kMinClass << c;
-        std::lock_guard<std::mutex> g(mu);
-        if (!free_by_class[c].empty()) {
-            uint8_t *p = free_by_class[c].back();
-            free_by_class[c].pop_back();
-            return p;
-        }
-        if (sz > kChunk) {  // (no plan table is this large; served directly)
-            void *p = nullptr;
-            if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
-            chunks.push_back(p);
-            return (uint8_t *)p;
-        }
-        if (left < sz) {
-            void *p = nullptr;
-            if (hipMalloc(&p, kChunk) != hipSuccess) return nullptr;
-            chunks.push_back(p);
-            cur = (uint8_t *)p;
-            left = kChunk;
-        }
-        uint8_t *p = cur;
-        cur += sz;
-        left -= sz;
-        return p;
-    }
-    void release(uint8_t *p, size_t n) {
-        if (!p) return;
-        std::lock_guard<std::mutex> g(mu);
-        free_by_class[cls(n)].push_back(p);
-    }
-    ~DevArena() {
-        for (void *p : chunks) (void)hipFree(p);
-    }
-};
+// This file: the context, plans, encode, rebuild, per-stripe calls, the host
+// pipeline, hashing, Decode with correction.  ec_sets.cpp: the share-set
+// calls and the background builder of straight-line code.  ec_upload.cpp: the
+// streamed upload.  ec_internal.hpp: what the three share.
+#include "ec_internal.hpp"
 
-// Completion marks of a context's runtime-matrix launches, per caller stream.
-// Each launch gets the next sequence number of its stream; an event is
-// recorded behind every kEvery-th launch only (a marker on the stream costs
-// microseconds per launch).  Launch q on stream s is known complete once an
-// event recorded at or after it has completed.  Events are recorded only at
-// launch time, on the stream being launched on, and queried afterwards (never
-// recorded on a stream the caller may have destroyed since).
-struct StreamMarks {
-    static constexpr int kEvery = 8;
-    static constexpr size_t kMaxStreams = 32;
-    struct Mark {
-        hipStream_t s = nullptr;
-        uint64_t issued = 0, ev_seq = 0;
-        int since = 0;
-        hipEvent_t ev = nullptr;
-    };
-    std::mutex mu;
-    std::deque<Mark> marks;  // most recently used streams last
-    // note a launch just queued on s; returns its sequence number (0: untracked)
-    uint64_t launched(hipStream_t s) {
-        std::lock_guard<std::mutex> g(mu);
-        Mark *m = nullptr;
-        for (auto it = marks.begin(); it != marks.end(); ++it)
-            if (it->s == s) {
-                if (std::next(it) != marks.end()) {  // most recently used last: eviction takes the idlest
-                    Mark keep = *it;
-                    marks.erase(it);
-                    marks.push_back(keep);
-                }
-                m = &marks.back();
-                break;
-            }
-        if (!m) {
-            if (marks.size() >= kMaxStreams) {  // the least recently used stream's marks go
-                if (marks.front().ev) (void)hipEventDestroy(marks.front().ev);
-                marks.pop_front();
-            }
-            marks.emplace_back();
-            m = &marks.back();
-            m->s = s;
-            if (hipEventCreateWithFlags(&m->ev, hipEventDisableTiming) != hipSuccess) m->ev = nullptr;
-        }
-        const uint64_t q = ++m->issued;
-        if (++m->since >= kEvery && m->ev && hipEventRecord(m->ev, s) == hipSuccess) {
-            m->since = 0;
-            m->ev_seq = q;
-        }
-        return q;
-    }
-    bool done(hipStream_t s, uint64_t q) {
-        std::lock_guard<std::mutex> g(mu);
-        for (auto &x : marks)
-            if (x.s == s) return q != 0 && x.ev && x.ev_seq >= q && hipEventQuery(x.ev) == hipSuccess;
-        return false;
-    }
-    ~StreamMarks() {
-        for (auto &x : marks)
-            if (x.ev) (void)hipEventSynchronize(x.ev), (void)hipEventDestroy(x.ev);
-    }
-};
+#pragma GCC visibility push(hidden)  // (the library's internals: not in its dynamic symbol table)
+namespace uplink_ec {
+namespace capi {
 
-struct MatPlan {
-    std::shared_ptr<DevArena> arena;  // where d_coef, d_tgt and d_sl live
-    std::shared_ptr<StreamMarks> marks;  // the context's completion marks
-    size_t coef_bytes = 0, sl_bytes = 0;
-    std::vector<size_t> tgt_bytes;
-    std::atomic<int> launches{0};     // launches made with this plan (straight-line code from the second on)
-    std::vector<int> key;          // what the matrix is (decode: chosen share ids; see plan keys below)
-    std::vector<int> missing;      // decode plans: the data positions rebuilt, in row order
-    int rows = 0, nin = 0, coef_ld = 0;
-    uint8_t *d_coef = nullptr;     // [j][r], ld = coef_ld
-    std::vector<uint64_t *> d_tgt; // leaf addresses per block of kMaxOps rows
-    std::vector<uint8_t> M;        // rows x nin, row-major (for the straight-line code)
-    std::mutex sl_mu;
-    bool sl_tried = false;
-    std::atomic<bool> sl_ready{false};  // d_sl is set (launch paths read this, not d_sl, without sl_mu)
-    hipModule_t sl_mod = nullptr;
-    uint64_t *d_sl = nullptr;      // segment addresses [pass][chunk][group]
-    // The plan's launches, as (stream, sequence number) of the context's
-    // completion marks: the latest per stream.  A plan is destroyed only when
-    // every one of them is known complete (evicted plans wait in the context's
-    // graveyard for that); if not -- its last reference went elsewhere, or the
-    // marks were dropped -- the destructor synchronises the device instead.
-    std::mutex use_mu;
-    std::vector<std::pair<hipStream_t, uint64_t>> uses;
-    void note_use(hipStream_t s) {
-        const uint64_t q = marks ? marks->launched(s) : 0;
-        std::lock_guard<std::mutex> g(use_mu);
-        for (auto &u : uses)
-            if (u.first == s) {
-                u.second = q;
-                return;
-            }
-        uses.emplace_back(s, q);
-    }
-    bool idle() {
-        std::lock_guard<std::mutex> g(use_mu);
-        for (auto &u : uses)
-            if (!marks || !marks->done(u.first, u.second)) return false;
-        return true;
-    }
-    ~MatPlan() {
-        if (!uses.empty() && !idle()) (void)hipDeviceSynchronize();
-        if (arena) {
-            arena->release(d_coef, coef_bytes);
-            for (size_t i = 0; i < d_tgt.size(); i++) arena->release((uint8_t *)d_tgt[i], tgt_bytes[i]);
-            arena->release((uint8_t *)d_sl, sl_bytes);
-        }
-        if (sl_mod) (void)hipModuleUnload(sl_mod);
-    }
-};
-using PlanPtr = std::shared_ptr<MatPlan>;
-
-struct Workspace {
-    uint8_t *d_buf = nullptr;
-    size_t cap = 0;
-    uint8_t *h_buf = nullptr;  // pinned staging for the per-stripe calls' host buffers
-    size_t h_cap = 0;
-    hipStream_t stream = nullptr;
-};
-
-// A caller waiting for a workspace (acquire_ws).
-struct WsWaiter {
-    std::condition_variable cv;
-    Workspace *w = nullptr;
-};
-
-// EncodeSingle requests waiting for a batched launch (ec_encode_single).
-struct SingleReq {
-    const uint8_t *in;
-    size_t bs;
-    uint8_t *out;
-    int num;
-    int rc = EC_OK;
-    bool taken = false;  // in a batch a leader is running
-    bool done = false;
-    std::condition_variable cv;  // this caller's wake-up (done, or its turn to lead)
-};
-
-// Every export that takes a context runs on the context's device and
-// restores the caller's current device on return (a Go caller's goroutine
-// may move between OS threads, each with its own current device).
-struct DeviceGuard {
-    int prev = -1;
-    bool switched = false;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) == hipSuccess && prev != dev) switched = hipSetDevice(dev) == hipSuccess;
-    }
-    ~DeviceGuard() {
-        if (switched) (void)hipSetDevice(prev);
-    }
-};
-
-}  // namespace
-
-struct HostPipe {
-    static constexpr int kSlots = 3;
-    hipStream_t st[kSlots] = {};
-    uint8_t *d_in[kSlots] = {};
-    uint8_t *d_out[kSlots] = {};
-    size_t in_cap = 0, out_cap = 0;
-};
-
-// Device side of one streamed upload (ec_upload_begin): the segment, its
-// pieces and the four role streams (H2D, encode, D2H, piece hashes).  Kept in
-// a per-context pool between uploads; one upload owns a slot from begin to end.
-struct UploadSlot {
-    hipStream_t st[4] = {};
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    size_t in_cap = 0, out_cap = 0;
-    uint8_t *d_hash = nullptr;   // EC_FLAG_HASH_PIECES: chunk CVs | hashes | fold scratch
-    size_t hash_cap = 0;
-    uint8_t *h_hash = nullptr;   // pinned, n*32 bytes: the hashes as they come back
-    size_t h_hash_cap = 0;
-    std::vector<hipEvent_t> ev;  // [in ch][enc ch][d2h ch][hashes] of the current upload
-    ~UploadSlot() {  // (also on an error path of ec_upload_begin: nothing of it is left behind)
-        for (auto st : this->st)
-            if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
-        for (auto e : ev)
-            if (e) (void)hipEventDestroy(e);
-        if (d_in) (void)hipFree(d_in);
-        if (d_out) (void)hipFree(d_out);
-        if (d_hash) (void)hipFree(d_hash);
-        if (h_hash) (void)hipHostFree(h_hash);
-    }
-};
-
-// One slot of a context's share-set calls (rs_sets.hpp): the pinned staging
-// the host writes, the device descriptors and leaf tables rs_sets_prep makes
-// from it, and the words the launches report through.  A call takes a slot
-// whose previous call has finished on the GPU -- its last workgroup stores the
-// call's sequence number into *h_done (pinned) -- so neither the host's writes
-// nor the prep kernel's ever overtake a launch still reading the slot, and no
-// event, marker or synchronisation is put on the caller's stream.
-struct SetsSlot {
-    SetStage *h_stage = nullptr;  // pinned, stage_cap entries (host-cached unless the zero-copy form)
-    SetStage *d_stage = nullptr;  // device copy of it (the DMA form: one hipMemcpyAsync per call)
-    size_t stage_cap = 0;
-    SetDesc *d_desc = nullptr;    // device, stage_cap entries
-    uint64_t *d_tgt = nullptr;    // device leaf tables, tgt_cap words
-    size_t tgt_cap = 0;
-    uint32_t *d_words = nullptr;  // device: [0] done counter, [1 + g] segment g's syndrome count (stage_cap + 1)
-    uint32_t *h_words = nullptr;  // pinned: [0] done sequence number, [1 + g] syndrome counts read back (Decode)
-    uint32_t seq = 0;             // of the slot's latest call
-    bool busy = false;            // a caller is filling or launching it
-    bool dead = false;            // a launch failed after the prep: never reused
-    ~SetsSlot() {
-        if (h_stage) (void)hipHostFree(h_stage);
-        if (d_stage) (void)hipFree(d_stage);
-        if (d_desc) (void)hipFree(d_desc);
-        if (d_tgt) (void)hipFree(d_tgt);
-        if (d_words) (void)hipFree(d_words);
-        if (h_words) (void)hipHostFree(h_words);
-    }
-    bool idle() const { return !busy && !dead && __atomic_load_n(h_words, __ATOMIC_ACQUIRE) == seq; }
-};
-
-struct SetsRing {
-    static constexpr size_t kMaxSlots = 16;  // calls in flight per context before a caller waits
-    std::mutex mu;
-    std::vector<std::unique_ptr<SetsSlot>> slots;
-};
-
-// Background maker of decode plans' straight-line code (DESIGN.md §4
-// "Straight-line rebuild bodies"): code generation and hipModuleLoadData take
-// ~0.4 ms per share set, so a batched rebuild never waits for them.  A launch
-// whose share set has no ready code runs the share-set path (jump-table body,
-// rs_sets.hpp) and queues the set here; later launches of the set take the
-// generated code once it has landed.
-struct SlBuilder {
-    std::mutex mu;
-    std::condition_variable cv;      // work queued / stop (worker), a set finished (waiters)
-    std::deque<std::vector<int>> q;  // share sets (chosen ids) to build
-    std::set<std::vector<int>> pending;
-    std::thread th;
-    bool stop = false;
-};
-
-// Work counters of the compile-time encoder's launches (RsArgs::queue): a
-// ring of counter pairs (tile counter, workgroups done), zeroed once when the
-// ring is made.  The last workgroup of a launch puts its pair back to zero
-// (rs_encoder.hpp), so a launch needs no memset before it, and then stores the
-// launch's sequence number into the slot's completion word in pinned host
-// memory.  A slot serves one launch at a time: it goes to a launch on the
-// stream its previous launch ran on (stream order), or to any stream once its
-// completion word shows that its latest launch has finished; with no such
-// slot the launch assigns its tiles statically (identical results).  No launch
-// waits on another stream and none needs an event or marker on its stream, so
-// a stream that launches a few times and goes away leaves its slot to the
-// others.
-struct QueueRing {
-    static constexpr int kSlots = 32;
-    static constexpr int kStride = 64;  // words per slot: the counter pair (kQueueDoneWord), a slot per 256 bytes
-    std::mutex mu;
-    uint32_t *d = nullptr;
-    uint32_t *h_done = nullptr;         // pinned, coherent: [slot] sequence number of its latest finished launch
-    uint32_t seq[kSlots] = {};          // [slot] sequence number of its latest launch
-    hipStream_t owner[kSlots] = {};     // stream of the slot's last launch
-    bool used[kSlots] = {}, busy[kSlots] = {};
-    bool done(int i) const { return __atomic_load_n(h_done + i, __ATOMIC_ACQUIRE) == seq[i]; }
-};
-
-struct ec_ctx {
-    int k = 0, n = 0, ess = 0, device = 0;
-    QueueRing qring;
-    std::atomic<uint64_t> q_taken{0}, q_static{0};  // encoder launches with a counter slot / static tiles
-    std::mutex pipe_mu;  // one host pipeline at a time per context
-    HostPipe pipe;
-    std::mutex upload_mu;
-    std::vector<std::unique_ptr<UploadSlot>> upload_free;  // idle streamed-upload slots
-    std::vector<uint8_t> G;        // n x k
-    hipStream_t setup = nullptr;   // plan uploads (synchronous, never a caller's stream)
-    std::shared_ptr<DevArena> arena = std::make_shared<DevArena>();
-    std::shared_ptr<StreamMarks> marks = std::make_shared<StreamMarks>();
-    std::vector<PlanPtr> graveyard;  // evicted plans whose launches may still run (under mu)
-    std::mutex setup_mu;
-    std::mutex mu;
-    std::list<PlanPtr> plans;      // decode / re-encode plans, MRU first
-    PlanPtr enc_parity;            // rows k..n-1 of G
-    std::vector<PlanPtr> enc_row;  // row num of G (EncodeSingle)
-    std::vector<Workspace *> free_ws;
-    std::vector<std::unique_ptr<Workspace>> all_ws;
-    std::deque<WsWaiter *> ws_waiters;  // callers waiting for a workspace, first come first served
-    uint32_t *d_chk = nullptr;     // checked build: the kernels' violation word
-    int body = EC_BODY_AUTO;       // ec_set_body
-    int last_body = EC_BODY_AUTO;  // ec_last_body
-    // EncodeSingle coalescing (group commit): callers queue; up to
-    // kSingleLeaders of them at a time each run everything queued as one batch
-    std::mutex single_mu;
-    std::deque<SingleReq *> single_q;
-    int single_leaders = 0;
-    // fault injection for tests only (UPLINK_EC_FAULT_SINGLE="max=M,num=J" read
-    // at ec_create): EncodeSingle batches of more than M requests find no
-    // staging, nor does a one-request batch for share J
-    int fault_max_batch = 0, fault_fail_num = -1;
-    // share-set calls (ec_*_segments_sets, and fresh share sets of the batched rebuild)
-    uint64_t jt_base = 0;          // address of the jump table's leaf 0 on this device
-    // one launch per share-set call on the widest class's waves, instead of one per wave-count
-    // class: 951.2 vs 982.6 us per 32 fresh-set segments on one box (profiles/r05/d/bench_sets*.json);
-    // UPLINK_EC_SETS_MERGE=0 at ec_create for the per-class launches (A/B)
-    bool sets_merge = true;
-    // the per-segment staging is read by the prep kernel straight from coherent pinned memory, or
-    // -- UPLINK_EC_SETS_STAGE_DMA=1 -- reaches the GPU by one DMA into device memory per call (host
-    // writes to cached pinned memory; the stream then waits ~20 us for the copy engine between
-    // calls, profiles/r05/g)
-    bool sets_stage_dma = false;
-    SetsRing sets;
-    SlBuilder slb;
-};
-
-namespace {
 
 constexpr size_t kMaxPlans = 64;
 // coefficient rows are read as whole 32-bit words past the last row (OPW slots)
@@ -423,11 +30,6 @@ int hip_fail(hipError_t e) {
     return EC_ERR_DEVICE;
 }
 
-#define HIP_TRY(x)                                   \
-    do {                                             \
-        hipError_t e_ = (x);                         \
-        if (e_ != hipSuccess) return hip_fail(e_);   \
-    } while (0)
 
 // At most kMaxWorkspaces per context: each has its own stream, and beyond a
 // few the streams only share the device's hardware queues (GPU_MAX_HW_QUEUES,
@@ -730,10 +332,6 @@ void queue_done(ec_ctx *c, hipStream_t s, int slot, uint32_t seq, bool launched)
     q.busy[slot] = false;
 }
 
-// Launches of at least this many tiles use a plan's straight-line code under
-// EC_BODY_AUTO: its module costs a code generation and a module load once per
-// plan, which only pays over many stripes.
-constexpr int64_t kSlMinTiles = 64;
 
 // Whole-segment encodes with at most this many parity rows run on the
 // parity plan's straight-line code instead of a compile-time encoder: one
@@ -934,380 +532,12 @@ int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const
                              s);
 }
 
-// ---------------------------------------------------------------- share-set calls (rs_sets.hpp)
-
-// One segment of a share-set call as the host prepares it: the inputs in the
-// kernel's order (infectious' k chosen shares by position, then -- Decode --
-// the other shares by number) and the rows (missing data positions, then one
-// syndrome row per non-basis input).
-struct SetSeg {
-    const uint8_t *in[kMaxOps];
-    int num[kMaxOps];
-    int missing[kMaxOps];
-    int nin = 0, nstore = 0, rows = 0, nw = 2;
-    uint8_t *out = nullptr;
-};
-
-// Fill `sg` for one segment given as (nshares, nums, pieces).  Errors as
-// Rebuild / Decode report them (NotEnoughShares, invalid share id, a repeated
-// share chosen twice: singular).
-int set_segment(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, uint8_t *out,
-                bool decode, SetSeg &sg) {
-    const int k = c->k;
-    std::vector<int> order, ids;
-    int rc = choose_shares(c, nshares, nums, order, ids);
-    if (rc) return rc;
-    if (decode)
-        for (int i = 0; i < nshares; i++)
-            if (nums[i] < 0 || nums[i] >= c->n) return EC_ERR_INVALID_SHARE;
-    bool seen[256] = {};
-    sg.nin = k;
-    sg.nstore = 0;
-    for (int i = 0; i < k; i++) {
-        if (seen[ids[i]]) return EC_ERR_SINGULAR;
-        seen[ids[i]] = true;
-        sg.in[i] = pieces[order[i]];
-        sg.num[i] = ids[i];
-        if (ids[i] >= k) sg.missing[sg.nstore++] = i;
-    }
-    if (decode) {
-        if (nshares > kMaxOps) return EC_ERR_UNSUPPORTED;
-        std::vector<char> chosen(nshares, 0);
-        for (int i = 0; i < k; i++) chosen[order[i]] = 1;
-        std::vector<int> rest;
-        for (int i = 0; i < nshares; i++)
-            if (!chosen[i]) rest.push_back(i);
-        std::stable_sort(rest.begin(), rest.end(), [&](int x, int y) { return nums[x] < nums[y]; });
-        for (int i : rest) {
-            sg.in[sg.nin] = pieces[i];
-            sg.num[sg.nin++] = nums[i];
-        }
-    }
-    sg.rows = sg.nstore + (sg.nin - k);
-    sg.nw = sets_waves(sg.rows);
-    sg.out = out;
-    return EC_OK;
-}
-
-// The slots' host memory is read by rs_sets_prep and written by the launches'
-// last workgroup straight over the bus: coherent (uncached on the GPU side), so
-// a slot reused by the next call is never read from a stale cache line.
-constexpr unsigned kSetsHostFlags = hipHostMallocCoherent | hipHostMallocMapped;
-
-// A free slot of the ring with room for nseg segments and tgt_words words of
-// leaf tables (waits while kMaxSlots calls are in flight on the GPU).
-SetsSlot *sets_acquire(ec_ctx *c, size_t nseg, size_t tgt_words) {
-    SetsRing &R = c->sets;
-    SetsSlot *sl = nullptr;
-    for (;;) {
-        {
-            std::lock_guard<std::mutex> g(R.mu);
-            for (auto &x : R.slots)
-                if (x->idle()) {
-                    sl = x.get();
-                    break;
-                }
-            if (!sl && R.slots.size() < SetsRing::kMaxSlots) {
-                auto x = std::make_unique<SetsSlot>();
-                if (hipHostMalloc((void **)&x->h_words, 4 * 65, kSetsHostFlags) != hipSuccess) return nullptr;
-                memset(x->h_words, 0, 4 * 65);
-                x->stage_cap = 0;
-                R.slots.push_back(std::move(x));
-                sl = R.slots.back().get();
-            }
-            if (sl) sl->busy = true;
-        }
-        if (sl) break;
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-    // (the slot is ours, and the GPU is done with it: its buffers may be replaced)
-    bool ok = true;
-    if (sl->stage_cap < nseg) {
-        const size_t cap = std::max<size_t>(32, (nseg + 31) & ~(size_t)31);
-        if (sl->h_stage) (void)hipHostFree(sl->h_stage);
-        if (sl->d_stage) (void)hipFree(sl->d_stage);
-        if (sl->d_desc) (void)hipFree(sl->d_desc);
-        if (sl->d_words) (void)hipFree(sl->d_words);
-        sl->h_stage = nullptr, sl->d_stage = nullptr, sl->d_desc = nullptr, sl->d_words = nullptr;
-        ok = hipHostMalloc((void **)&sl->h_stage, cap * sizeof(SetStage),
-                           c->sets_stage_dma ? hipHostMallocDefault : kSetsHostFlags) == hipSuccess &&
-             (!c->sets_stage_dma || hipMalloc(&sl->d_stage, cap * sizeof(SetStage)) == hipSuccess) &&
-             hipMalloc(&sl->d_desc, cap * sizeof(SetDesc)) == hipSuccess &&
-             hipMalloc(&sl->d_words, 4 * (cap + 1)) == hipSuccess;
-        if (ok && cap + 1 > 65) {
-            uint32_t *hw = nullptr;
-            ok = hipHostMalloc((void **)&hw, 4 * (cap + 1), kSetsHostFlags) == hipSuccess;
-            if (ok) {
-                hw[0] = sl->seq;
-                (void)hipHostFree(sl->h_words);
-                sl->h_words = hw;
-            }
-        }
-        sl->stage_cap = ok ? cap : 0;
-    }
-    if (ok && sl->tgt_cap < tgt_words) {
-        const size_t cap = std::max<size_t>(tgt_words, (size_t)32 * 8192);
-        if (sl->d_tgt) (void)hipFree(sl->d_tgt);
-        sl->d_tgt = nullptr;
-        ok = hipMalloc(&sl->d_tgt, cap * 8) == hipSuccess;
-        sl->tgt_cap = ok ? cap : 0;
-    }
-    if (!ok) {
-        std::lock_guard<std::mutex> g(R.mu);
-        sl->busy = false;
-        return nullptr;
-    }
-    return sl;
-}
-
-void sets_release(ec_ctx *c, SetsSlot *sl) {
-    std::lock_guard<std::mutex> g(c->sets.mu);
-    sl->busy = false;
-}
-
-// The share-set pass over segs (each nstripes stripes): rs_sets_prep, then one
-// rs_matmul_sets launch per wave-count class, all on stream s.  With `bad`
-// (Decode), waits and returns per segment the count of syndrome failures.
-int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_t s, std::vector<uint32_t> *bad) {
-    const int k = c->k, ess = c->ess;
-    const size_t nseg = segs.size();
-    if (nseg == 0 || nstripes == 0) return EC_OK;
-    if (c->sets_merge) {  // every segment on the widest class's workgroups: one launch, one tail
-        int nw = 2;
-        for (auto &sg : segs) nw = std::max(nw, sg.nw);
-        for (auto &sg : segs) sg.nw = nw;
-    }
-    {  // more tiles than one launch takes: in parts (each a call of its own)
-        const int64_t tiles_seg = (nstripes * (ess / 16) + kTileChunksHost - 1) / kTileChunksHost;
-        const int64_t per = sets_max_tiles(4) / tiles_seg;
-        if (per < 1) return EC_ERR_UNSUPPORTED;
-        if ((int64_t)nseg > per) {
-            for (size_t g0 = 0; g0 < nseg; g0 += (size_t)per) {
-                std::vector<SetSeg> part(segs.begin() + g0, segs.begin() + std::min(nseg, g0 + (size_t)per));
-                std::vector<uint32_t> pbad;
-                const int rc = sets_call(c, part, nstripes, s, bad ? &pbad : nullptr);
-                if (rc) return rc;
-                if (bad) bad->insert(bad->end(), pbad.begin(), pbad.end());
-            }
-            return EC_OK;
-        }
-    }
-    std::vector<int> idx(nseg);
-    for (size_t g = 0; g < nseg; g++) idx[g] = (int)g;
-    std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return segs[x].nw < segs[y].nw; });
-    std::vector<size_t> toff(nseg);
-    size_t words = 0;
-    for (size_t q = 0; q < nseg; q++) {
-        toff[q] = words;
-        words += (sets_tgt_entries(segs[idx[q]].nin, segs[idx[q]].rows, segs[idx[q]].nw) + 7) & ~(size_t)7;
-    }
-    SetsSlot *sl = sets_acquire(c, nseg, words);
-    if (!sl) return EC_ERR_DEVICE;
-    for (size_t q = 0; q < nseg; q++) {
-        const SetSeg &sg = segs[idx[q]];
-        SetStage &st = sl->h_stage[q];
-        SetDesc &d = st.d;
-        for (int j = 0; j < sg.nin; j++) {
-            d.in[j] = sg.in[j];
-            d.copy_off[j] = j < k && sg.num[j] < k ? sg.num[j] * ess : -1;
-            st.num[j] = sg.num[j];
-        }
-        for (int r = 0; r < sg.nstore; r++) {
-            d.out_off[r] = sg.missing[r] * ess;
-            st.missing[r] = sg.missing[r];
-        }
-        d.out = sg.out;
-        d.tgt = sl->d_tgt + toff[q];
-        d.zero_check = bad ? sl->d_words + 1 + q : nullptr;
-        d.nin = sg.nin;
-        d.nout = sg.rows;
-        d.nstore = sg.nstore;
-        d.status = 0;
-        st.k = k;
-        st.nw = sg.nw;
-    }
-    const uint32_t seq = sl->seq + 1;
-    const int64_t chunks = nstripes * (ess / 16), tiles = (chunks + kTileChunksHost - 1) / kTileChunksHost;
-    hipError_t e = hipSuccess;
-    if (sl->d_stage)  // (the host's writes went to cached memory; one DMA takes them to the device)
-        e = hipMemcpyAsync(sl->d_stage, sl->h_stage, nseg * sizeof(SetStage), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = launch_sets_prep(sl->d_stage ? sl->d_stage : sl->h_stage, sl->d_desc, (int)nseg, c->jt_base, sl->d_words,
-                             s);
-    if (e != hipSuccess) {  // nothing was queued: the slot is as it was
-        sets_release(c, sl);
-        return hip_fail(e);
-    }
-    for (size_t q0 = 0; q0 < nseg && e == hipSuccess;) {
-        size_t q1 = q0;
-        while (q1 < nseg && segs[idx[q1]].nw == segs[idx[q0]].nw) q1++;
-        SetsArgs a{};
-        a.desc = sl->d_desc + q0;
-        a.nstripes = nstripes;
-        a.chunks_per_seg = chunks;
-        a.tiles_per_seg = tiles;
-        a.total_tiles = tiles * (int64_t)(q1 - q0);
-        a.ess = ess;
-        a.cps = ess / 16;
-        a.k = k;
-        a.done_ctr = sl->d_words;
-        a.host_done = sl->h_words;
-        a.seq = seq;
-        a.total_wgs = (uint32_t)(tiles * (int64_t)nseg);
-        a.chk_flag = c->d_chk;
-        e = launch_matmul_sets(a, segs[idx[q0]].nw, s);
-        q0 = q1;
-    }
-    if (e != hipSuccess) {  // the slot may be half used: never again
-        std::lock_guard<std::mutex> g(c->sets.mu);
-        sl->dead = true;
-        sl->busy = false;
-        return hip_fail(e);
-    }
-    sl->seq = seq;
-    c->last_body = EC_BODY_JUMP_TABLE;
-    int rc = after_launch(c->d_chk, s);
-    if (bad && rc == EC_OK) {
-        // (the slot stays busy until the counts are read: another call may not reuse it before)
-        if (hipMemcpyAsync(sl->h_words + 1, sl->d_words + 1, 4 * nseg, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            rc = EC_ERR_DEVICE;
-        bad->assign(nseg, 0);
-        for (size_t q = 0; q < nseg && rc == EC_OK; q++) (*bad)[idx[q]] = sl->h_words[1 + q];
-    }
-    sets_release(c, sl);
-    return rc;
-}
-
-// ---------------------------------------------------------------- straight-line code in the background
-
-std::mutex g_builders_mu;
-std::set<ec_ctx *> g_builders;  // contexts whose builder thread runs
-
-void sl_worker(ec_ctx *c) {
-    (void)hipSetDevice(c->device);
-    SlBuilder &B = c->slb;
-    for (;;) {
-        std::vector<int> ids;
-        {
-            std::unique_lock<std::mutex> g(B.mu);
-            B.cv.wait(g, [&] { return B.stop || !B.q.empty(); });
-            if (B.stop) break;
-            ids = std::move(B.q.front());
-            B.q.pop_front();
-        }
-        PlanPtr plan;
-        if (get_plan(c, ids, &plan) == EC_OK && plan->rows >= 1 && plan->rows <= kMaxOps) ensure_sl(c, *plan);
-        {
-            std::lock_guard<std::mutex> g(B.mu);
-            B.pending.erase(ids);
-        }
-        B.cv.notify_all();
-    }
-    std::lock_guard<std::mutex> g(B.mu);
-    B.pending.clear();
-    B.q.clear();
-    B.cv.notify_all();
-}
-
-// At exit, builders still running finish the plan in hand before the HIP
-// runtime's own exit handlers (registered before this one, on the first HIP
-// call) tear the runtime down under a module load.
-void stop_builders() {
-    std::lock_guard<std::mutex> g(g_builders_mu);
-    for (ec_ctx *c : g_builders) {
-        {
-            std::lock_guard<std::mutex> b(c->slb.mu);
-            c->slb.stop = true;
-        }
-        c->slb.cv.notify_all();
-        if (c->slb.th.joinable()) c->slb.th.join();
-    }
-    g_builders.clear();
-}
-
-void stop_builder(ec_ctx *c) {
-    {
-        std::lock_guard<std::mutex> g(g_builders_mu);
-        g_builders.erase(c);
-        {
-            std::lock_guard<std::mutex> b(c->slb.mu);
-            c->slb.stop = true;
-        }
-        c->slb.cv.notify_all();
-    }
-    if (c->slb.th.joinable()) c->slb.th.join();
-}
-
-// Queue the straight-line code of share set `ids` (no-op if queued already).
-void sl_request(ec_ctx *c, const std::vector<int> &ids) {
-    SlBuilder &B = c->slb;
-    std::lock_guard<std::mutex> g(B.mu);
-    if (B.stop || B.pending.count(ids)) return;
-    if (!B.th.joinable()) {
-        static std::once_flag once;
-        std::call_once(once, [] { atexit(stop_builders); });
-        std::lock_guard<std::mutex> r(g_builders_mu);
-        B.th = std::thread(sl_worker, c);
-        g_builders.insert(c);
-    }
-    B.pending.insert(ids);
-    B.q.push_back(ids);
-    B.cv.notify_all();
-}
-
-// The context's plan for share set ids, if it has one (no plan is made).
-PlanPtr find_plan(ec_ctx *c, const std::vector<int> &ids) {
-    std::lock_guard<std::mutex> g(c->mu);
-    for (auto it = c->plans.begin(); it != c->plans.end(); ++it)
-        if ((*it)->key == ids) {
-            c->plans.splice(c->plans.begin(), c->plans, it);
-            return c->plans.front();
-        }
-    return nullptr;
-}
-
-// The batched rebuild as ec_rebuild_segments_batched runs it: nothing on the
-// launch path waits for the host or another stream.  A share set whose
-// straight-line code is ready runs it; any other runs the share-set pass (its
-// decode rows solved on the GPU, stream-ordered) and, for launches large
-// enough to use it, has its code made in the background.
-int rebuild_async(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int64_t nstripes,
-                  int64_t nseg, int64_t pss, int64_t oss, uint8_t *out, hipStream_t s) {
-    const int k = c->k, ess = c->ess;
-    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
-    std::vector<int> order, ids;
-    int rc = choose_shares(c, nshares, nums, order, ids);
-    if (rc) return rc;
-    bool bits = ess % 16 == 0 && aligned16(out) && pss % 16 == 0 && oss % 16 == 0;
-    int m = 0;
-    for (int i = 0; i < k; i++) {
-        bits = bits && aligned16(pieces[order[i]]);
-        m += ids[i] >= k;
-    }
-    // byte kernel, forced straight-line code, or nothing to compute (the copy
-    // kernel; its plan has no tables to wait for): the plan path
-    if (!bits || m == 0 || c->body == EC_BODY_STRAIGHT_LINE)
-        return rebuild_device(c, nshares, nums, pieces, ess, nstripes, nseg, pss, oss, out, s);
-    const int64_t tiles = (nstripes * (ess / 16) + kTileChunksHost - 1) / kTileChunksHost * nseg;
-    if (c->body == EC_BODY_AUTO && tiles >= kSlMinTiles) {
-        if (PlanPtr plan = find_plan(c, ids); plan && plan->sl_ready.load(std::memory_order_acquire))
-            return rebuild_with_plan(c, *plan, order, ids, pieces, ess, nstripes, nseg, pss, oss, out, s);
-        sl_request(c, ids);
-    }
-    std::vector<SetSeg> segs(nseg);
-    std::vector<const uint8_t *> pg(nshares);
-    for (int64_t g = 0; g < nseg; g++) {
-        for (int i = 0; i < nshares; i++) pg[i] = pieces[i] + g * pss;
-        rc = set_segment(c, nshares, nums, pg.data(), out + g * oss, false, segs[g]);
-        if (rc) return rc;
-    }
-    return sets_call(c, segs, nstripes, s, nullptr);
-}
-
-}  // namespace
+}  // namespace capi
+}  // namespace uplink_ec
+#pragma GCC visibility pop
 
 extern "C" {
+
 
 int ec_set_body(ec_ctx *c, int body) {
     if (!c || body < EC_BODY_AUTO || body > EC_BODY_STRAIGHT_LINE) return EC_ERR_INVALID_ARG;
@@ -1485,7 +715,10 @@ int ec_prepare_encoder(const ec_ctx *c, int wait) {
 // pieces keep their full layout ([seg][rows][nstripes*ess]), the range
 // writes its part of every piece (used to pipeline one segment through PCIe
 // in chunks of stripes).
-static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, size_t s0, size_t s1,
+}  // extern "C"
+namespace uplink_ec {
+namespace capi {
+int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, size_t s0, size_t s1,
                         uint8_t *pieces, int flags, hipStream_t s) {
     if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
     if (nseg == 0 || s1 <= s0) return EC_OK;
@@ -1538,6 +771,9 @@ static int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstr
     if (rc) return rc;
     return run_matmul(c, a, out_off.data(), *plan, (int64_t)nseg, bits, s);
 }
+}  // namespace capi
+}  // namespace uplink_ec
+extern "C" {
 
 int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
                        int flags, ec_stream stream) {
@@ -1545,110 +781,6 @@ int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_
     DeviceGuard dg(cc->device);
     return encode_range(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, 0, nstripes, pieces, flags,
                         (hipStream_t)stream);
-}
-
-int ec_rebuild_segments_batched(const ec_ctx *cc, int nshares, const int *nums, const uint8_t *const *pieces,
-                                size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
-                                uint8_t *out, ec_stream stream) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
-    if (!c || !nums || !pieces || !out) return EC_ERR_INVALID_ARG;
-    if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
-    if (nstripes == 0 || nseg == 0) return EC_OK;
-    DeviceGuard dg(c->device);
-    return rebuild_async(c, nshares, nums, pieces, (int64_t)nstripes, (int64_t)nseg, piece_seg_stride, out_seg_stride,
-                         out, (hipStream_t)stream);
-}
-
-// Segment g's shares are entries [off_g, off_g + nshares[g]) of nums / pieces.
-static int sets_export(ec_ctx *c, size_t nseg, const int *nshares, const int *nums, const uint8_t *const *pieces,
-                       size_t nstripes, uint8_t *const *outs, hipStream_t s, bool decode) {
-    const int ess = c->ess;
-    if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
-    // a call of many segments goes in passes of at most kPass (bounded staging per slot)
-    constexpr size_t kPass = 64;
-    std::vector<SetSeg> segs;
-    std::vector<size_t> seg_of;  // segs[i] is segment seg_of[i] of the call
-    std::vector<size_t> off(nseg + 1, 0);
-    for (size_t g = 0; g < nseg; g++) off[g + 1] = off[g] + (size_t)std::max(nshares[g], 0);
-    auto flush = [&]() -> int {
-        std::vector<uint32_t> bad;
-        int rc = sets_call(c, segs, (int64_t)nstripes, s, decode ? &bad : nullptr);
-        // Decode: a segment whose syndromes are not all zero is corrected (in the
-        // caller's pieces, as infectious corrects share.Data) and rebuilt on its own
-        for (size_t i = 0; i < segs.size() && rc == EC_OK && decode; i++)
-            if (bad[i]) {
-                const size_t g = seg_of[i];
-                rc = ec_decode_segments(c, nshares[g], nums + off[g], (uint8_t *const *)pieces + off[g], nstripes,
-                                        outs[g], (ec_stream)s);
-            }
-        segs.clear();
-        seg_of.clear();
-        return rc;
-    };
-    for (size_t g = 0; g < nseg; g++) {
-        const int ns = nshares[g];
-        if (ns < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
-        bool bits = ess % 16 == 0 && aligned16(outs[g]) && (!decode || ns <= kMaxOps);
-        for (int i = 0; i < ns; i++) bits = bits && aligned16(pieces[off[g] + i]);
-        if (!bits) {  // byte kernel / more inputs than a launch takes: this segment on its own
-            const int rc = decode ? ec_decode_segments(c, ns, nums + off[g], (uint8_t *const *)pieces + off[g], nstripes,
-                                                       outs[g], (ec_stream)s)
-                                  : rebuild_device(c, ns, nums + off[g], pieces + off[g], ess, (int64_t)nstripes, 1,
-                                                   0, 0, outs[g], s);
-            if (rc) return rc;
-            continue;
-        }
-        segs.emplace_back();
-        seg_of.push_back(g);
-        if (int rc = set_segment(c, ns, nums + off[g], pieces + off[g], outs[g], decode, segs.back())) return rc;
-        if (segs.size() == kPass)
-            if (int rc = flush()) return rc;
-    }
-    return segs.empty() ? EC_OK : flush();
-}
-
-int ec_rebuild_segments_sets(const ec_ctx *cc, size_t nseg, const int *nshares, const int *nums,
-                             const uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
-    if (!c || (nseg && (!nshares || !nums || !pieces || !outs))) return EC_ERR_INVALID_ARG;
-    if (nseg == 0 || nstripes == 0) return EC_OK;
-    for (size_t g = 0; g < nseg; g++)
-        if (!outs[g]) return EC_ERR_INVALID_ARG;
-    DeviceGuard dg(c->device);
-    return sets_export(c, nseg, nshares, nums, pieces, nstripes, outs, (hipStream_t)stream, false);
-}
-
-int ec_decode_segments_sets(const ec_ctx *cc, size_t nseg, const int *nshares, const int *nums,
-                            uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
-    if (!c || (nseg && (!nshares || !nums || !pieces || !outs))) return EC_ERR_INVALID_ARG;
-    if (nseg == 0 || nstripes == 0) return EC_OK;
-    for (size_t g = 0; g < nseg; g++)
-        if (!outs[g]) return EC_ERR_INVALID_ARG;
-    DeviceGuard dg(c->device);
-    int rc = sets_export(c, nseg, nshares, nums, (const uint8_t *const *)pieces, nstripes, outs, (hipStream_t)stream,
-                         true);
-    if (rc == EC_OK && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = EC_ERR_DEVICE;
-    return rc;
-}
-
-int ec_prepare_rebuild(const ec_ctx *cc, int nshares, const int *nums, int wait) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
-    if (!c || !nums) return EC_ERR_INVALID_ARG;
-    DeviceGuard dg(c->device);
-    std::vector<int> order, ids;
-    if (int rc = choose_shares(c, nshares, nums, order, ids)) return rc;
-    int m = 0;
-    for (int i = 0; i < c->k; i++) m += ids[i] >= c->k;
-    if (m == 0 || c->k > kMaxOps || c->ess % 16) return 0;  // (no code to make: copies, or the byte kernel)
-    if (PlanPtr p = find_plan(c, ids); p && p->sl_ready.load(std::memory_order_acquire)) return 1;
-    sl_request(c, ids);
-    if (wait) {
-        std::unique_lock<std::mutex> g(c->slb.mu);
-        c->slb.cv.wait(g, [&] { return c->slb.pending.count(ids) == 0; });
-    }
-    PlanPtr p = find_plan(c, ids);
-    return p && p->sl_ready.load(std::memory_order_acquire) ? 1 : 0;
 }
 
 int ec_rebuild_segments(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces,
@@ -1686,7 +818,13 @@ static int pipe_drain(ec_ctx *c, int rc) {
     return rc;
 }
 
-static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // extern "C"
+namespace uplink_ec {
+namespace capi {
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // namespace capi
+}  // namespace uplink_ec
+extern "C" {
 
 // ---------------------------------------------------------------- per-stripe
 // single_batch_once: one launch sequence for the whole batch, or kSplit when
@@ -1962,21 +1100,24 @@ void ec_host_free(void *p) {
 // hashes [nseg][n][32]: the data pieces of all nseg segments in one launch,
 // the parity pieces in another; the hash rows of a segment are n*32 apart,
 // so each launch writes into a [nseg][rows][32] staging area first.
-static B3View data_view(const ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes) {
+}  // extern "C"
+namespace uplink_ec {
+namespace capi {
+B3View data_view(const ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes) {
     const uint64_t plen = nstripes * (uint64_t)c->ess;
     return B3View{segs, (int64_t)c->ess, plen, (uint64_t)c->ess, (int64_t)c->k * c->ess, nseg * (uint64_t)c->k,
                   (uint64_t)c->k, (int64_t)(plen * c->k), 0};
 }
-static B3View parity_view(const ec_ctx *c, const uint8_t *parity, size_t nseg, size_t nstripes) {
+B3View parity_view(const ec_ctx *c, const uint8_t *parity, size_t nseg, size_t nstripes) {
     const uint64_t plen = nstripes * (uint64_t)c->ess;
     return B3View{parity, (int64_t)plen, plen, plen, (int64_t)plen, nseg * (uint64_t)(c->n - c->k), 0, 0, 0};
 }
-static size_t b3_segment_ws_bytes(const ec_ctx *c, size_t nseg, size_t nstripes) {
+size_t b3_segment_ws_bytes(const ec_ctx *c, size_t nseg, size_t nstripes) {
     B3View all = parity_view(c, nullptr, nseg, nstripes);
     all.npieces = nseg * (uint64_t)c->n;
     return align_up(b3_workspace_bytes(all), 256) + align_up(32 * nseg * (size_t)c->n, 256);
 }
-static int hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,
+int hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,
                          uint8_t *hashes, uint8_t *ws, hipStream_t st) {
     const size_t n = c->n, k = c->k;
     uint8_t *stage = ws;  // [data: nseg*k*32][parity: nseg*(n-k)*32]
@@ -1991,6 +1132,9 @@ static int hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *pa
                                  hipMemcpyDeviceToDevice, st));
     return EC_OK;
 }
+}  // namespace capi
+}  // namespace uplink_ec
+extern "C" {
 
 // Host pipeline of the encode.  The three pipe streams take roles (H2D,
 // compute, D2H) and every segment goes through in chunks of stripes, so the
@@ -2073,303 +1217,6 @@ int ec_encode_segments_host_hashed(const ec_ctx *cc, const uint8_t *segs, size_t
                                    uint8_t *pieces, uint8_t *hashes, int flags) {
     if (!hashes) return EC_ERR_INVALID_ARG;
     return encode_host(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, pieces, hashes, flags);
-}
-
-// ---------------------------------------------------------------- streamed upload
-// One segment through the engine in chunks of stripes, each chunk of every
-// piece in host memory as soon as it is encoded, for piece readers that serve
-// a piece stripe by stripe (segmentupload/encode.go:39-75, single.go:228-238):
-// an upload starts sending after the first chunk instead of the whole segment.
-// Chunks grow from kUploadFirstChunk stripes, doubling up to kUploadMaxChunk,
-// so the first bytes come early and the later chunks keep the PCIe pipeline
-// (H2D of chunk i+1, encode of chunk i, D2H of chunk i-1) busy.
-constexpr size_t kUploadFirstChunk = 128, kUploadMaxChunk = 2048;
-
-struct ec_upload {
-    ec_ctx *c = nullptr;
-    std::unique_ptr<UploadSlot> slot;
-    std::vector<size_t> end;  // end stripe of each chunk
-    std::atomic<int> rc{EC_OK};
-    std::atomic<int> done{0};  // leading chunks known to be in host memory
-    int n = 0;                 // pieces hashed (EC_FLAG_HASH_PIECES), 0 without
-    // the hash work, queued by the first caller that waits on the upload or asks for the hashes
-    // (not by ec_upload_begin, so the first chunk's copies and encode start without waiting for
-    // the host to queue ~10 more operations)
-    std::once_flag hash_once;
-    int hash_rc = EC_OK;
-    bool streamed_hash = false, parity_only = false;
-    size_t nstripes = 0;
-    B3View dv{}, pv{};
-    uint32_t *cvs = nullptr;
-    uint8_t *d_hashes = nullptr, *d_scratch = nullptr, *d_parity = nullptr;
-    // ec_upload_end waits for the callers inside ec_upload_wait / _ready /
-    // _hashes before it frees the handle (piece readers block in
-    // those while another thread closes the segment)
-    std::mutex mu;
-    std::condition_variable cv;
-    int inside = 0;
-    bool ending = false;
-};
-
-static void upload_release(ec_upload *u) {
-    if (!u->slot) return;
-    for (auto st : u->slot->st)
-        if (st) (void)hipStreamSynchronize(st);
-    std::lock_guard<std::mutex> g(u->c->upload_mu);
-    u->c->upload_free.push_back(std::move(u->slot));
-}
-
-// A caller inside one of the waiting calls on u (released by the destructor).
-struct UploadUse {
-    ec_upload *u;
-    bool ok;
-    explicit UploadUse(ec_upload *x) : u(x) {
-        std::lock_guard<std::mutex> g(u->mu);
-        ok = !u->ending;
-        if (ok) u->inside++;
-    }
-    ~UploadUse() {
-        if (!ok) return;
-        std::lock_guard<std::mutex> g(u->mu);
-        if (--u->inside == 0) u->cv.notify_all();
-    }
-};
-
-// The piece hashes of a streamed upload, chunk by chunk: after the encode of
-// each chunk of stripes, the chaining values of the BLAKE3 chunks that chunk
-// completes in every piece (data pieces straight from the segment, parity from
-// the encoder's output), on a stream of their own; after the last, the tree
-// fold and the hashes' copy to pinned memory.  The reference hashes each piece
-// as it streams through a TeeReader and needs the sum only at the end
-// (piecestore/upload.go:155,262-270): so does this.  A chunk boundary that
-// does not fall on a 1-KiB boundary of the pieces (a caller's chunk size), or
-// pieces of one BLAKE3 chunk, hash everything after the last chunk instead.
-static bool upload_hash_streamed(const ec_ctx *c, const std::vector<size_t> &end, size_t nstripes) {
-    const uint64_t plen = (uint64_t)nstripes * c->ess;
-    if (plen < 2048) return false;
-    for (size_t i = 0; i + 1 < end.size(); i++)
-        if ((end[i] * (uint64_t)c->ess) % 1024) return false;
-    return true;
-}
-
-int ec_upload_begin(const ec_ctx *cc, const uint8_t *seg, size_t nstripes, uint8_t *pieces, int flags,
-                    size_t chunk_stripes, ec_upload **out) {
-    ec_ctx *c = const_cast<ec_ctx *>(cc);
-    if (!out) return EC_ERR_INVALID_ARG;
-    *out = nullptr;
-    if (!c || !seg || !pieces) return EC_ERR_INVALID_ARG;
-    if (flags & ~(EC_FLAG_PARITY_ONLY | EC_FLAG_HASH_PIECES)) return EC_ERR_INVALID_ARG;
-    DeviceGuard dg(c->device);
-    std::unique_ptr<ec_upload> u(new ec_upload());
-    u->c = c;
-    for (size_t s0 = 0, len = chunk_stripes ? chunk_stripes : kUploadFirstChunk; s0 < nstripes;) {
-        const size_t s1 = std::min(nstripes, s0 + len);
-        u->end.push_back(s1);
-        s0 = s1;
-        if (!chunk_stripes) len = std::min(kUploadMaxChunk, 2 * len);
-    }
-    const size_t nch = u->end.size();
-    const size_t ess = c->ess, stripe = (size_t)c->k * ess, spad = nstripes * stripe;
-    const bool parity_only = (flags & EC_FLAG_PARITY_ONLY) != 0;
-    const bool hashed = (flags & EC_FLAG_HASH_PIECES) != 0;
-    const int rows = parity_only ? c->n - c->k : c->n;
-    const size_t plen = nstripes * ess, pbytes = (size_t)rows * plen;
-    const bool streamed_hash = hashed && upload_hash_streamed(c, u->end, nstripes);
-    const uint64_t nb3 = (plen + 1023) / 1024;  // BLAKE3 chunks per piece
-    // hash area: [n][nb3][8] chunk CVs | n*32 hashes | scratch (fold, or the one-pass hash's)
-    const size_t cvs_bytes = streamed_hash ? align_up((size_t)c->n * nb3 * 32, 256) : 0;
-    const size_t hash_bytes = align_up(32 * (size_t)c->n, 256);
-    const size_t scratch = streamed_hash ? b3_fold_ws_bytes(c->n, nb3) : b3_segment_ws_bytes(c, 1, nstripes);
-    const size_t hcap = hashed ? cvs_bytes + hash_bytes + std::max<size_t>(scratch, 256) : 0;
-    {
-        std::lock_guard<std::mutex> g(c->upload_mu);
-        if (!c->upload_free.empty()) {
-            u->slot = std::move(c->upload_free.back());
-            c->upload_free.pop_back();
-        }
-    }
-    if (!u->slot) u->slot.reset(new UploadSlot());
-    UploadSlot &sl = *u->slot;
-    for (auto &st : sl.st)
-        if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    if (sl.in_cap < spad) {
-        if (sl.d_in) (void)hipFree(sl.d_in);
-        sl.d_in = nullptr;
-        sl.in_cap = 0;
-        HIP_TRY(hipMalloc(&sl.d_in, std::max<size_t>(spad, 1)));
-        sl.in_cap = spad;
-    }
-    if (sl.out_cap < pbytes) {
-        if (sl.d_out) (void)hipFree(sl.d_out);
-        sl.d_out = nullptr;
-        sl.out_cap = 0;
-        HIP_TRY(hipMalloc(&sl.d_out, std::max<size_t>(pbytes, 1)));
-        sl.out_cap = pbytes;
-    }
-    if (hashed && sl.hash_cap < hcap) {
-        if (sl.d_hash) (void)hipFree(sl.d_hash);
-        sl.d_hash = nullptr;
-        sl.hash_cap = 0;
-        HIP_TRY(hipMalloc(&sl.d_hash, hcap));
-        sl.hash_cap = hcap;
-    }
-    if (hashed && sl.h_hash_cap < 32 * (size_t)c->n) {
-        if (sl.h_hash) (void)hipHostFree(sl.h_hash);
-        sl.h_hash = nullptr;
-        sl.h_hash_cap = 0;
-        HIP_TRY(hipHostMalloc((void **)&sl.h_hash, 32 * (size_t)c->n, hipHostMallocDefault));
-        sl.h_hash_cap = 32 * (size_t)c->n;
-    }
-    while (sl.ev.size() < 3 * nch + 1) {
-        hipEvent_t e = nullptr;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        sl.ev.push_back(e);
-    }
-    hipStream_t h2d = sl.st[0], comp = sl.st[1], d2h = sl.st[2];
-    uint32_t *cvs = (uint32_t *)sl.d_hash;
-    uint8_t *d_hashes = sl.d_hash + cvs_bytes, *d_scratch = d_hashes + hash_bytes;
-    const uint8_t *d_parity = sl.d_out + (parity_only ? 0 : (size_t)c->k * plen);
-    B3View pv = parity_view(c, d_parity, 1, nstripes);
-    if (c->n == c->k) pv.npieces = 0;
-    const B3View dv = data_view(c, sl.d_in, 1, nstripes);
-    int rc = EC_OK;
-    for (size_t ch = 0; ch < nch && rc == EC_OK; ch++) {
-        const size_t s0 = ch ? u->end[ch - 1] : 0, s1 = u->end[ch];
-        hipEvent_t e_in = sl.ev[ch], e_enc = sl.ev[nch + ch], e_out = sl.ev[2 * nch + ch];
-        if (hipMemcpyAsync(sl.d_in + s0 * stripe, seg + s0 * stripe, (s1 - s0) * stripe, hipMemcpyHostToDevice,
-                           h2d) != hipSuccess ||
-            hipEventRecord(e_in, h2d) != hipSuccess || hipStreamWaitEvent(comp, e_in, 0) != hipSuccess) {
-            rc = EC_ERR_DEVICE;
-            break;
-        }
-        if (rows > 0) rc = encode_range(c, sl.d_in, 1, nstripes, s0, s1, sl.d_out, flags & EC_FLAG_PARITY_ONLY, comp);
-        if (rc) break;
-        if (hipEventRecord(e_enc, comp) != hipSuccess || hipStreamWaitEvent(d2h, e_enc, 0) != hipSuccess ||
-            (rows > 0 && hipMemcpy2DAsync(pieces + s0 * ess, plen, sl.d_out + s0 * ess, plen, (s1 - s0) * ess, rows,
-                                          hipMemcpyDeviceToHost, d2h) != hipSuccess) ||
-            hipEventRecord(e_out, d2h) != hipSuccess)
-            rc = EC_ERR_DEVICE;
-    }
-    if (hashed) {  // queued later (upload_queue_hashes): the first chunk is not held up by it
-        u->n = c->n;
-        u->streamed_hash = streamed_hash;
-        u->parity_only = parity_only;
-        u->nstripes = nstripes;
-        u->dv = dv;
-        u->pv = pv;
-        u->cvs = cvs;
-        u->d_hashes = d_hashes;
-        u->d_scratch = d_scratch;
-        u->d_parity = (uint8_t *)d_parity;
-    }
-    u->rc.store(rc);
-    if (rc) {
-        upload_release(u.get());
-        return rc;
-    }
-    *out = u.release();
-    return EC_OK;
-}
-
-// The piece-hash work of an EC_FLAG_HASH_PIECES upload, on its hash stream:
-// each group of about a third of the chunks hashed as soon as its last chunk
-// is encoded (a stream wait on that chunk's encode event), then the tree fold
-// and the hashes' copy to pinned memory.  Queued once, by the first caller of
-// ec_upload_wait or ec_upload_hashes.
-static void upload_queue_hashes(ec_upload *u) {
-    std::call_once(u->hash_once, [u] {
-        ec_ctx *c = u->c;
-        UploadSlot &sl = *u->slot;
-        const size_t nch = u->end.size(), ess = c->ess;
-        const uint64_t nb3 = (u->nstripes * ess + 1023) / 1024;
-        hipStream_t hs = sl.st[3];
-        hipError_t e = hipSuccess;
-        if (u->streamed_hash) {
-            size_t from = 0;  // first stripe not yet hashed
-            for (size_t ch = 0; ch < nch && e == hipSuccess; ch++) {
-                const bool last = ch + 1 == nch;
-                if (!last && (u->end[ch] - from) * 3 < u->nstripes) continue;  // (groups of ~1/3 of the segment)
-                const uint64_t c0 = from * ess / 1024, c1 = last ? nb3 : u->end[ch] * ess / 1024;
-                e = hipStreamWaitEvent(hs, sl.ev[nch + ch], 0);
-                if (e == hipSuccess) e = b3_launch_chunk_range(u->dv, u->pv, c0, c1, u->cvs, hs);
-                from = u->end[ch];
-            }
-        }
-        if (e == hipSuccess) e = hipStreamWaitEvent(hs, sl.ev[2 * nch - 1], 0);  // (the last encode)
-        if (e == hipSuccess)
-            e = u->streamed_hash ? b3_launch_fold(u->cvs, c->n, nb3, u->d_hashes, u->d_scratch, hs)
-                                 : (hash_segments(c, sl.d_in, u->d_parity, 1, u->nstripes, u->d_hashes, u->d_scratch,
-                                                  hs) == EC_OK ? hipSuccess : hipErrorUnknown);
-        if (e == hipSuccess) e = hipMemcpyAsync(sl.h_hash, u->d_hashes, 32 * (size_t)c->n, hipMemcpyDeviceToHost, hs);
-        if (e == hipSuccess) e = hipEventRecord(sl.ev[3 * nch], hs);
-        u->hash_rc = e == hipSuccess ? EC_OK : hip_fail(e);
-    });
-}
-
-static int upload_wait_chunks(ec_upload *u, size_t stripes) {
-    const int nch = (int)u->end.size();
-    for (;;) {
-        if (const int rc = u->rc.load()) return rc;
-        int d = u->done.load();
-        if (d == nch || (d > 0 && u->end[d - 1] >= stripes)) return EC_OK;
-        if (hipEventSynchronize(u->slot->ev[2 * nch + d]) != hipSuccess) {
-            u->rc.store(EC_ERR_DEVICE);
-            return EC_ERR_DEVICE;
-        }
-        u->done.compare_exchange_strong(d, d + 1);
-    }
-}
-
-// Any number of threads may wait on one upload (one per piece reader); the
-// event waits run without a lock, and the count of done chunks only grows.
-int ec_upload_wait(ec_upload *u, size_t stripes) {
-    if (!u) return EC_ERR_INVALID_ARG;
-    UploadUse use(u);
-    if (!use.ok) return EC_ERR_INVALID_ARG;
-    DeviceGuard dg(u->c->device);
-    if (u->n && u->rc.load() == EC_OK) upload_queue_hashes(u);  // (while the first chunk is on its way)
-    return upload_wait_chunks(u, stripes);
-}
-
-size_t ec_upload_ready(ec_upload *u) {
-    if (!u || u->rc.load()) return 0;
-    UploadUse use(u);
-    if (!use.ok) return 0;
-    DeviceGuard dg(u->c->device);
-    const int nch = (int)u->end.size();
-    for (int d = u->done.load(); d < nch && hipEventQuery(u->slot->ev[2 * nch + d]) == hipSuccess; d = u->done.load())
-        u->done.compare_exchange_strong(d, d + 1);
-    const int d = u->done.load();
-    return d ? u->end[d - 1] : 0;
-}
-
-int ec_upload_hashes(ec_upload *u, uint8_t *hashes) {
-    if (!u || !hashes) return EC_ERR_INVALID_ARG;
-    UploadUse use(u);
-    if (!use.ok || u->n == 0) return EC_ERR_INVALID_ARG;  // (begun without EC_FLAG_HASH_PIECES)
-    if (const int rc = u->rc.load()) return rc;
-    DeviceGuard dg(u->c->device);
-    upload_queue_hashes(u);
-    if (u->hash_rc) return u->hash_rc;
-    if (hipEventSynchronize(u->slot->ev[3 * u->end.size()]) != hipSuccess) return EC_ERR_DEVICE;
-    memcpy(hashes, u->slot->h_hash, 32 * (size_t)u->n);
-    return EC_OK;
-}
-
-int ec_upload_end(ec_upload *u) {
-    if (!u) return EC_ERR_INVALID_ARG;
-    int rc = u->rc.load();
-    {
-        DeviceGuard dg(u->c->device);
-        if (rc == EC_OK) rc = upload_wait_chunks(u, SIZE_MAX);
-        std::unique_lock<std::mutex> g(u->mu);
-        u->ending = true;  // new callers are turned away; those inside finish first
-        u->cv.wait(g, [&] { return u->inside == 0; });
-        g.unlock();
-        upload_release(u);
-    }
-    delete u;
-    return rc;
 }
 
 int ec_hash_segments(const ec_ctx *c, const uint8_t *segs, const uint8_t *parity, size_t nseg, size_t nstripes,

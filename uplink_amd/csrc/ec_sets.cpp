@@ -1,0 +1,496 @@
+// C-ABI, share-set calls (include/uplink_ec.h ec_rebuild_segments_sets,
+// ec_decode_segments_sets, ec_rebuild_segments_batched, ec_prepare_rebuild):
+// a batch of segments each rebuilt or decoded from its own share set in one
+// stream-ordered pass (rs_sets.hpp), and the per-context background builder
+// of decode plans' straight-line code.
+#include "ec_internal.hpp"
+
+namespace uplink_ec {
+namespace capi {
+namespace {
+
+// ---------------------------------------------------------------- share-set calls (rs_sets.hpp)
+
+// One segment of a share-set call as the host prepares it: the inputs in the
+// kernel's order (infectious' k chosen shares by position, then -- Decode --
+// the other shares by number) and the rows (missing data positions, then one
+// syndrome row per non-basis input).
+struct SetSeg {
+    const uint8_t *in[kMaxOps];
+    int num[kMaxOps];
+    int missing[kMaxOps];
+    int nin = 0, nstore = 0, rows = 0, nw = 2;
+    uint8_t *out = nullptr;
+};
+
+// Fill `sg` for one segment given as (nshares, nums, pieces).  Errors as
+// Rebuild / Decode report them (NotEnoughShares, invalid share id, a repeated
+// share chosen twice: singular).
+int set_segment(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, uint8_t *out,
+                bool decode, SetSeg &sg) {
+    const int k = c->k;
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    if (decode)
+        for (int i = 0; i < nshares; i++)
+            if (nums[i] < 0 || nums[i] >= c->n) return EC_ERR_INVALID_SHARE;
+    bool seen[256] = {};
+    sg.nin = k;
+    sg.nstore = 0;
+    for (int i = 0; i < k; i++) {
+        if (seen[ids[i]]) return EC_ERR_SINGULAR;
+        seen[ids[i]] = true;
+        sg.in[i] = pieces[order[i]];
+        sg.num[i] = ids[i];
+        if (ids[i] >= k) sg.missing[sg.nstore++] = i;
+    }
+    if (decode) {
+        if (nshares > kMaxOps) return EC_ERR_UNSUPPORTED;
+        std::vector<char> chosen(nshares, 0);
+        for (int i = 0; i < k; i++) chosen[order[i]] = 1;
+        std::vector<int> rest;
+        for (int i = 0; i < nshares; i++)
+            if (!chosen[i]) rest.push_back(i);
+        std::stable_sort(rest.begin(), rest.end(), [&](int x, int y) { return nums[x] < nums[y]; });
+        for (int i : rest) {
+            sg.in[sg.nin] = pieces[i];
+            sg.num[sg.nin++] = nums[i];
+        }
+    }
+    sg.rows = sg.nstore + (sg.nin - k);
+    sg.nw = sets_waves(sg.rows);
+    sg.out = out;
+    return EC_OK;
+}
+
+// The slots' host memory is read by rs_sets_prep and written by the launches'
+// last workgroup straight over the bus: coherent (uncached on the GPU side), so
+// a slot reused by the next call is never read from a stale cache line.
+constexpr unsigned kSetsHostFlags = hipHostMallocCoherent | hipHostMallocMapped;
+
+// A free slot of the ring with room for nseg segments and tgt_words words of
+// leaf tables (waits while kMaxSlots calls are in flight on the GPU).
+SetsSlot *sets_acquire(ec_ctx *c, size_t nseg, size_t tgt_words) {
+    SetsRing &R = c->sets;
+    SetsSlot *sl = nullptr;
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(R.mu);
+            for (auto &x : R.slots)
+                if (x->idle()) {
+                    sl = x.get();
+                    break;
+                }
+            if (!sl && R.slots.size() < SetsRing::kMaxSlots) {
+                auto x = std::make_unique<SetsSlot>();
+                if (hipHostMalloc((void **)&x->h_words, 4 * 65, kSetsHostFlags) != hipSuccess) return nullptr;
+                memset(x->h_words, 0, 4 * 65);
+                x->stage_cap = 0;
+                R.slots.push_back(std::move(x));
+                sl = R.slots.back().get();
+            }
+            if (sl) sl->busy = true;
+        }
+        if (sl) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    // (the slot is ours, and the GPU is done with it: its buffers may be replaced)
+    bool ok = true;
+    if (sl->stage_cap < nseg) {
+        const size_t cap = std::max<size_t>(32, (nseg + 31) & ~(size_t)31);
+        if (sl->h_stage) (void)hipHostFree(sl->h_stage);
+        if (sl->d_stage) (void)hipFree(sl->d_stage);
+        if (sl->d_desc) (void)hipFree(sl->d_desc);
+        if (sl->d_words) (void)hipFree(sl->d_words);
+        sl->h_stage = nullptr, sl->d_stage = nullptr, sl->d_desc = nullptr, sl->d_words = nullptr;
+        ok = hipHostMalloc((void **)&sl->h_stage, cap * sizeof(SetStage),
+                           c->sets_stage_dma ? hipHostMallocDefault : kSetsHostFlags) == hipSuccess &&
+             (!c->sets_stage_dma || hipMalloc(&sl->d_stage, cap * sizeof(SetStage)) == hipSuccess) &&
+             hipMalloc(&sl->d_desc, cap * sizeof(SetDesc)) == hipSuccess &&
+             hipMalloc(&sl->d_words, 4 * (cap + 1)) == hipSuccess;
+        if (ok && cap + 1 > 65) {
+            uint32_t *hw = nullptr;
+            ok = hipHostMalloc((void **)&hw, 4 * (cap + 1), kSetsHostFlags) == hipSuccess;
+            if (ok) {
+                hw[0] = sl->seq;
+                (void)hipHostFree(sl->h_words);
+                sl->h_words = hw;
+            }
+        }
+        sl->stage_cap = ok ? cap : 0;
+    }
+    if (ok && sl->tgt_cap < tgt_words) {
+        const size_t cap = std::max<size_t>(tgt_words, (size_t)32 * 8192);
+        if (sl->d_tgt) (void)hipFree(sl->d_tgt);
+        sl->d_tgt = nullptr;
+        ok = hipMalloc(&sl->d_tgt, cap * 8) == hipSuccess;
+        sl->tgt_cap = ok ? cap : 0;
+    }
+    if (!ok) {
+        std::lock_guard<std::mutex> g(R.mu);
+        sl->busy = false;
+        return nullptr;
+    }
+    return sl;
+}
+
+void sets_release(ec_ctx *c, SetsSlot *sl) {
+    std::lock_guard<std::mutex> g(c->sets.mu);
+    sl->busy = false;
+}
+
+// The share-set pass over segs (each nstripes stripes): rs_sets_prep, then one
+// rs_matmul_sets launch per wave-count class, all on stream s.  With `bad`
+// (Decode), waits and returns per segment the count of syndrome failures.
+int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_t s, std::vector<uint32_t> *bad) {
+    const int k = c->k, ess = c->ess;
+    const size_t nseg = segs.size();
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    if (c->sets_merge) {  // every segment on the widest class's workgroups: one launch, one tail
+        int nw = 2;
+        for (auto &sg : segs) nw = std::max(nw, sg.nw);
+        for (auto &sg : segs) sg.nw = nw;
+    }
+    {  // more tiles than one launch takes: in parts (each a call of its own)
+        const int64_t tiles_seg = (nstripes * (ess / 16) + kTileChunksHost - 1) / kTileChunksHost;
+        const int64_t per = sets_max_tiles(4) / tiles_seg;
+        if (per < 1) return EC_ERR_UNSUPPORTED;
+        if ((int64_t)nseg > per) {
+            for (size_t g0 = 0; g0 < nseg; g0 += (size_t)per) {
+                std::vector<SetSeg> part(segs.begin() + g0, segs.begin() + std::min(nseg, g0 + (size_t)per));
+                std::vector<uint32_t> pbad;
+                const int rc = sets_call(c, part, nstripes, s, bad ? &pbad : nullptr);
+                if (rc) return rc;
+                if (bad) bad->insert(bad->end(), pbad.begin(), pbad.end());
+            }
+            return EC_OK;
+        }
+    }
+    std::vector<int> idx(nseg);
+    for (size_t g = 0; g < nseg; g++) idx[g] = (int)g;
+    std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return segs[x].nw < segs[y].nw; });
+    std::vector<size_t> toff(nseg);
+    size_t words = 0;
+    for (size_t q = 0; q < nseg; q++) {
+        toff[q] = words;
+        words += (sets_tgt_entries(segs[idx[q]].nin, segs[idx[q]].rows, segs[idx[q]].nw) + 7) & ~(size_t)7;
+    }
+    SetsSlot *sl = sets_acquire(c, nseg, words);
+    if (!sl) return EC_ERR_DEVICE;
+    for (size_t q = 0; q < nseg; q++) {
+        const SetSeg &sg = segs[idx[q]];
+        SetStage &st = sl->h_stage[q];
+        SetDesc &d = st.d;
+        for (int j = 0; j < sg.nin; j++) {
+            d.in[j] = sg.in[j];
+            d.copy_off[j] = j < k && sg.num[j] < k ? sg.num[j] * ess : -1;
+            st.num[j] = sg.num[j];
+        }
+        for (int r = 0; r < sg.nstore; r++) {
+            d.out_off[r] = sg.missing[r] * ess;
+            st.missing[r] = sg.missing[r];
+        }
+        d.out = sg.out;
+        d.tgt = sl->d_tgt + toff[q];
+        d.zero_check = bad ? sl->d_words + 1 + q : nullptr;
+        d.nin = sg.nin;
+        d.nout = sg.rows;
+        d.nstore = sg.nstore;
+        d.status = 0;
+        st.k = k;
+        st.nw = sg.nw;
+    }
+    const uint32_t seq = sl->seq + 1;
+    const int64_t chunks = nstripes * (ess / 16), tiles = (chunks + kTileChunksHost - 1) / kTileChunksHost;
+    hipError_t e = hipSuccess;
+    if (sl->d_stage)  // (the host's writes went to cached memory; one DMA takes them to the device)
+        e = hipMemcpyAsync(sl->d_stage, sl->h_stage, nseg * sizeof(SetStage), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = launch_sets_prep(sl->d_stage ? sl->d_stage : sl->h_stage, sl->d_desc, (int)nseg, c->jt_base, sl->d_words,
+                             s);
+    if (e != hipSuccess) {  // nothing was queued: the slot is as it was
+        sets_release(c, sl);
+        return hip_fail(e);
+    }
+    for (size_t q0 = 0; q0 < nseg && e == hipSuccess;) {
+        size_t q1 = q0;
+        while (q1 < nseg && segs[idx[q1]].nw == segs[idx[q0]].nw) q1++;
+        SetsArgs a{};
+        a.desc = sl->d_desc + q0;
+        a.nstripes = nstripes;
+        a.chunks_per_seg = chunks;
+        a.tiles_per_seg = tiles;
+        a.total_tiles = tiles * (int64_t)(q1 - q0);
+        a.ess = ess;
+        a.cps = ess / 16;
+        a.k = k;
+        a.done_ctr = sl->d_words;
+        a.host_done = sl->h_words;
+        a.seq = seq;
+        a.total_wgs = (uint32_t)(tiles * (int64_t)nseg);
+        a.chk_flag = c->d_chk;
+        e = launch_matmul_sets(a, segs[idx[q0]].nw, s);
+        q0 = q1;
+    }
+    if (e != hipSuccess) {  // the slot may be half used: never again
+        std::lock_guard<std::mutex> g(c->sets.mu);
+        sl->dead = true;
+        sl->busy = false;
+        return hip_fail(e);
+    }
+    sl->seq = seq;
+    c->last_body = EC_BODY_JUMP_TABLE;
+    int rc = after_launch(c->d_chk, s);
+    if (bad && rc == EC_OK) {
+        // (the slot stays busy until the counts are read: another call may not reuse it before)
+        if (hipMemcpyAsync(sl->h_words + 1, sl->d_words + 1, 4 * nseg, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = EC_ERR_DEVICE;
+        bad->assign(nseg, 0);
+        for (size_t q = 0; q < nseg && rc == EC_OK; q++) (*bad)[idx[q]] = sl->h_words[1 + q];
+    }
+    sets_release(c, sl);
+    return rc;
+}
+
+// ---------------------------------------------------------------- straight-line code in the background
+
+std::mutex g_builders_mu;
+std::set<ec_ctx *> g_builders;  // contexts whose builder thread runs
+
+void sl_worker(ec_ctx *c) {
+    (void)hipSetDevice(c->device);
+    SlBuilder &B = c->slb;
+    for (;;) {
+        std::vector<int> ids;
+        {
+            std::unique_lock<std::mutex> g(B.mu);
+            B.cv.wait(g, [&] { return B.stop || !B.q.empty(); });
+            if (B.stop) break;
+            ids = std::move(B.q.front());
+            B.q.pop_front();
+        }
+        PlanPtr plan;
+        if (get_plan(c, ids, &plan) == EC_OK && plan->rows >= 1 && plan->rows <= kMaxOps) ensure_sl(c, *plan);
+        {
+            std::lock_guard<std::mutex> g(B.mu);
+            B.pending.erase(ids);
+        }
+        B.cv.notify_all();
+    }
+    std::lock_guard<std::mutex> g(B.mu);
+    B.pending.clear();
+    B.q.clear();
+    B.cv.notify_all();
+}
+
+// At exit, builders still running finish the plan in hand before the HIP
+// runtime's own exit handlers (registered before this one, on the first HIP
+// call) tear the runtime down under a module load.
+void stop_builders() {
+    std::lock_guard<std::mutex> g(g_builders_mu);
+    for (ec_ctx *c : g_builders) {
+        {
+            std::lock_guard<std::mutex> b(c->slb.mu);
+            c->slb.stop = true;
+        }
+        c->slb.cv.notify_all();
+        if (c->slb.th.joinable()) c->slb.th.join();
+    }
+    g_builders.clear();
+}
+
+void stop_builder_impl(ec_ctx *c) {
+    {
+        std::lock_guard<std::mutex> g(g_builders_mu);
+        g_builders.erase(c);
+        {
+            std::lock_guard<std::mutex> b(c->slb.mu);
+            c->slb.stop = true;
+        }
+        c->slb.cv.notify_all();
+    }
+    if (c->slb.th.joinable()) c->slb.th.join();
+}
+
+// Queue the straight-line code of share set `ids` (no-op if queued already).
+void sl_request(ec_ctx *c, const std::vector<int> &ids) {
+    SlBuilder &B = c->slb;
+    std::lock_guard<std::mutex> g(B.mu);
+    if (B.stop || B.pending.count(ids)) return;
+    if (!B.th.joinable()) {
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(stop_builders); });
+        std::lock_guard<std::mutex> r(g_builders_mu);
+        B.th = std::thread(sl_worker, c);
+        g_builders.insert(c);
+    }
+    B.pending.insert(ids);
+    B.q.push_back(ids);
+    B.cv.notify_all();
+}
+
+// The context's plan for share set ids, if it has one (no plan is made).
+PlanPtr find_plan(ec_ctx *c, const std::vector<int> &ids) {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (auto it = c->plans.begin(); it != c->plans.end(); ++it)
+        if ((*it)->key == ids) {
+            c->plans.splice(c->plans.begin(), c->plans, it);
+            return c->plans.front();
+        }
+    return nullptr;
+}
+
+// The batched rebuild as ec_rebuild_segments_batched runs it: nothing on the
+// launch path waits for the host or another stream.  A share set whose
+// straight-line code is ready runs it; any other runs the share-set pass (its
+// decode rows solved on the GPU, stream-ordered) and, for launches large
+// enough to use it, has its code made in the background.
+int rebuild_async(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int64_t nstripes,
+                  int64_t nseg, int64_t pss, int64_t oss, uint8_t *out, hipStream_t s) {
+    const int k = c->k, ess = c->ess;
+    if (k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    std::vector<int> order, ids;
+    int rc = choose_shares(c, nshares, nums, order, ids);
+    if (rc) return rc;
+    bool bits = ess % 16 == 0 && aligned16(out) && pss % 16 == 0 && oss % 16 == 0;
+    int m = 0;
+    for (int i = 0; i < k; i++) {
+        bits = bits && aligned16(pieces[order[i]]);
+        m += ids[i] >= k;
+    }
+    // byte kernel, forced straight-line code, or nothing to compute (the copy
+    // kernel; its plan has no tables to wait for): the plan path
+    if (!bits || m == 0 || c->body == EC_BODY_STRAIGHT_LINE)
+        return rebuild_device(c, nshares, nums, pieces, ess, nstripes, nseg, pss, oss, out, s);
+    const int64_t tiles = (nstripes * (ess / 16) + kTileChunksHost - 1) / kTileChunksHost * nseg;
+    if (c->body == EC_BODY_AUTO && tiles >= kSlMinTiles) {
+        if (PlanPtr plan = find_plan(c, ids); plan && plan->sl_ready.load(std::memory_order_acquire))
+            return rebuild_with_plan(c, *plan, order, ids, pieces, ess, nstripes, nseg, pss, oss, out, s);
+        sl_request(c, ids);
+    }
+    std::vector<SetSeg> segs(nseg);
+    std::vector<const uint8_t *> pg(nshares);
+    for (int64_t g = 0; g < nseg; g++) {
+        for (int i = 0; i < nshares; i++) pg[i] = pieces[i] + g * pss;
+        rc = set_segment(c, nshares, nums, pg.data(), out + g * oss, false, segs[g]);
+        if (rc) return rc;
+    }
+    return sets_call(c, segs, nstripes, s, nullptr);
+}
+
+}  // namespace
+
+void stop_builder(ec_ctx *c) { stop_builder_impl(c); }
+
+}  // namespace capi
+}  // namespace uplink_ec
+
+extern "C" {
+
+int ec_rebuild_segments_batched(const ec_ctx *cc, int nshares, const int *nums, const uint8_t *const *pieces,
+                                size_t nstripes, size_t nseg, long long piece_seg_stride, long long out_seg_stride,
+                                uint8_t *out, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !nums || !pieces || !out) return EC_ERR_INVALID_ARG;
+    if (nshares < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+    if (nstripes == 0 || nseg == 0) return EC_OK;
+    DeviceGuard dg(c->device);
+    return rebuild_async(c, nshares, nums, pieces, (int64_t)nstripes, (int64_t)nseg, piece_seg_stride, out_seg_stride,
+                         out, (hipStream_t)stream);
+}
+
+// Segment g's shares are entries [off_g, off_g + nshares[g]) of nums / pieces.
+static int sets_export(ec_ctx *c, size_t nseg, const int *nshares, const int *nums, const uint8_t *const *pieces,
+                       size_t nstripes, uint8_t *const *outs, hipStream_t s, bool decode) {
+    const int ess = c->ess;
+    if (c->k > kMaxOps) return EC_ERR_UNSUPPORTED;
+    // a call of many segments goes in passes of at most kPass (bounded staging per slot)
+    constexpr size_t kPass = 64;
+    std::vector<SetSeg> segs;
+    std::vector<size_t> seg_of;  // segs[i] is segment seg_of[i] of the call
+    std::vector<size_t> off(nseg + 1, 0);
+    for (size_t g = 0; g < nseg; g++) off[g + 1] = off[g] + (size_t)std::max(nshares[g], 0);
+    auto flush = [&]() -> int {
+        std::vector<uint32_t> bad;
+        int rc = sets_call(c, segs, (int64_t)nstripes, s, decode ? &bad : nullptr);
+        // Decode: a segment whose syndromes are not all zero is corrected (in the
+        // caller's pieces, as infectious corrects share.Data) and rebuilt on its own
+        for (size_t i = 0; i < segs.size() && rc == EC_OK && decode; i++)
+            if (bad[i]) {
+                const size_t g = seg_of[i];
+                rc = ec_decode_segments(c, nshares[g], nums + off[g], (uint8_t *const *)pieces + off[g], nstripes,
+                                        outs[g], (ec_stream)s);
+            }
+        segs.clear();
+        seg_of.clear();
+        return rc;
+    };
+    for (size_t g = 0; g < nseg; g++) {
+        const int ns = nshares[g];
+        if (ns < c->k) return EC_ERR_NOT_ENOUGH_SHARES;
+        bool bits = ess % 16 == 0 && aligned16(outs[g]) && (!decode || ns <= kMaxOps);
+        for (int i = 0; i < ns; i++) bits = bits && aligned16(pieces[off[g] + i]);
+        if (!bits) {  // byte kernel / more inputs than a launch takes: this segment on its own
+            const int rc = decode ? ec_decode_segments(c, ns, nums + off[g], (uint8_t *const *)pieces + off[g], nstripes,
+                                                       outs[g], (ec_stream)s)
+                                  : rebuild_device(c, ns, nums + off[g], pieces + off[g], ess, (int64_t)nstripes, 1,
+                                                   0, 0, outs[g], s);
+            if (rc) return rc;
+            continue;
+        }
+        segs.emplace_back();
+        seg_of.push_back(g);
+        if (int rc = set_segment(c, ns, nums + off[g], pieces + off[g], outs[g], decode, segs.back())) return rc;
+        if (segs.size() == kPass)
+            if (int rc = flush()) return rc;
+    }
+    return segs.empty() ? EC_OK : flush();
+}
+
+int ec_rebuild_segments_sets(const ec_ctx *cc, size_t nseg, const int *nshares, const int *nums,
+                             const uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nseg && (!nshares || !nums || !pieces || !outs))) return EC_ERR_INVALID_ARG;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    for (size_t g = 0; g < nseg; g++)
+        if (!outs[g]) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    return sets_export(c, nseg, nshares, nums, pieces, nstripes, outs, (hipStream_t)stream, false);
+}
+
+int ec_decode_segments_sets(const ec_ctx *cc, size_t nseg, const int *nshares, const int *nums,
+                            uint8_t *const *pieces, size_t nstripes, uint8_t *const *outs, ec_stream stream) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || (nseg && (!nshares || !nums || !pieces || !outs))) return EC_ERR_INVALID_ARG;
+    if (nseg == 0 || nstripes == 0) return EC_OK;
+    for (size_t g = 0; g < nseg; g++)
+        if (!outs[g]) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    int rc = sets_export(c, nseg, nshares, nums, (const uint8_t *const *)pieces, nstripes, outs, (hipStream_t)stream,
+                         true);
+    if (rc == EC_OK && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) rc = EC_ERR_DEVICE;
+    return rc;
+}
+
+int ec_prepare_rebuild(const ec_ctx *cc, int nshares, const int *nums, int wait) {
+    ec_ctx *c = const_cast<ec_ctx *>(cc);
+    if (!c || !nums) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(c->device);
+    std::vector<int> order, ids;
+    if (int rc = choose_shares(c, nshares, nums, order, ids)) return rc;
+    int m = 0;
+    for (int i = 0; i < c->k; i++) m += ids[i] >= c->k;
+    if (m == 0 || c->k > kMaxOps || c->ess % 16) return 0;  // (no code to make: copies, or the byte kernel)
+    if (PlanPtr p = find_plan(c, ids); p && p->sl_ready.load(std::memory_order_acquire)) return 1;
+    sl_request(c, ids);
+    if (wait) {
+        std::unique_lock<std::mutex> g(c->slb.mu);
+        c->slb.cv.wait(g, [&] { return c->slb.pending.count(ids) == 0; });
+    }
+    PlanPtr p = find_plan(c, ids);
+    return p && p->sl_ready.load(std::memory_order_acquire) ? 1 : 0;
+}
+
+}  // extern "C"
