@@ -178,9 +178,13 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     }
     SetsSlot *sl = sets_acquire(c, nseg, words);
     if (!sl) return EC_ERR_DEVICE;
+    // one segment: its record goes in the prep launch's arguments (no read over the bus)
+    SetStage one{};
+    const bool in_args = nseg == 1 && !sl->d_stage;
+    SetStage *stage = in_args ? &one : sl->h_stage;
     for (size_t q = 0; q < nseg; q++) {
         const SetSeg &sg = segs[idx[q]];
-        SetStage &st = sl->h_stage[q];
+        SetStage &st = stage[q];
         SetDesc &d = st.d;
         for (int j = 0; j < sg.nin; j++) {
             d.in[j] = sg.in[j];
@@ -207,8 +211,9 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     if (sl->d_stage)  // (the host's writes went to cached memory; one DMA takes them to the device)
         e = hipMemcpyAsync(sl->d_stage, sl->h_stage, nseg * sizeof(SetStage), hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
-        e = launch_sets_prep(sl->d_stage ? sl->d_stage : sl->h_stage, sl->d_desc, (int)nseg, c->jt_base, sl->d_words,
-                             s);
+        e = in_args ? launch_sets_prep1(one, sl->d_desc, c->jt_base, sl->d_words, s)
+                    : launch_sets_prep(sl->d_stage ? sl->d_stage : sl->h_stage, sl->d_desc, (int)nseg, c->jt_base,
+                                       sl->d_words, s);
     if (e != hipSuccess) {  // nothing was queued: the slot is as it was
         sets_release(c, sl);
         return hip_fail(e);

@@ -47,8 +47,7 @@ __device__ __forceinline__ void rows_of(int pass, int npass, int nout, int nw, i
 
 __device__ __forceinline__ int npass_of(int nout, int nw) { return nout > 0 ? (nout + nw * kRows - 1) / (nw * kRows) : 1; }
 
-__global__ __launch_bounds__(256) void rs_sets_prep(const SetStage *stage, SetDesc *desc, uint64_t jt_base,
-                                                    uint32_t *done_ctr) {
+__device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64_t jt_base, uint32_t *done_ctr) {
     __shared__ uint8_t s_exp[512], s_log[256];
     __shared__ uint8_t s_x[kMaxOps];                    // basis points x_p
     __shared__ uint8_t s_y[2 * kMaxOps];                // row points y_r
@@ -59,9 +58,8 @@ __global__ __launch_bounds__(256) void rs_sets_prep(const SetStage *stage, SetDe
     __shared__ int s_hdr[8];
     __shared__ uint64_t *s_tgt;
     const int tid = threadIdx.x;
-    const SetStage *st = stage + blockIdx.x;
-    SetDesc *dd = desc + blockIdx.x;
-    // everything from the host's staging at once (one round trip over the bus)
+    // everything from the host's staging at once (one round trip over the bus, or the kernel's
+    // arguments)
     {
         const uint64_t *src = (const uint64_t *)&st->d;
         uint64_t *dst = (uint64_t *)dd;
@@ -140,6 +138,18 @@ __global__ __launch_bounds__(256) void rs_sets_prep(const SetStage *stage, SetDe
         }
         tgt[e] = jt_base + (uint64_t)c * RS_JT_SLOT;
     }
+}
+
+__global__ __launch_bounds__(256) void rs_sets_prep(const SetStage *stage, SetDesc *desc, uint64_t jt_base,
+                                                    uint32_t *done_ctr) {
+    prep_one(stage + blockIdx.x, desc + blockIdx.x, jt_base, done_ctr);
+}
+
+// One segment: its record passed as the kernel's argument (3.1 KB of the 4 KB a
+// launch carries), so the prep reads nothing over the bus
+__global__ __launch_bounds__(256) void rs_sets_prep1(const SetStage stage, SetDesc *desc, uint64_t jt_base,
+                                                     uint32_t *done_ctr) {
+    prep_one(&stage, desc, jt_base, done_ctr);
 }
 
 // checked build: every access of the tile stays inside its share / segment (one
@@ -311,6 +321,12 @@ hipError_t launch_sets_prep(const SetStage *stage, SetDesc *desc, int nseg, uint
                             hipStream_t s) {
     if (nseg <= 0) return hipSuccess;
     hipLaunchKernelGGL(rs_sets_prep, dim3(nseg), dim3(256), 0, s, stage, desc, jt_base, done_ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_sets_prep1(const SetStage &stage, SetDesc *desc, uint64_t jt_base, uint32_t *done_ctr,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(rs_sets_prep1, dim3(1), dim3(256), 0, s, stage, desc, jt_base, done_ctr);
     return hipGetLastError();
 }
 

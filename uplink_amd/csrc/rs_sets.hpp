@@ -69,6 +69,10 @@ int64_t sets_max_tiles(int nw);
 // zeroes *done_ctr for the launches that follow
 hipError_t launch_sets_prep(const SetStage *stage, SetDesc *desc, int nseg, uint64_t jt_base, uint32_t *done_ctr,
                             hipStream_t s);
+// the same for one segment, its record passed in the launch's arguments
+hipError_t launch_sets_prep1(const SetStage &stage, SetDesc *desc, uint64_t jt_base, uint32_t *done_ctr,
+                             hipStream_t s);
+static_assert(sizeof(SetStage) + 3 * sizeof(void *) <= 4096, "a launch's arguments are at most 4 KB");
 hipError_t launch_matmul_sets(const SetsArgs &a, int nw, hipStream_t s);
 // address of the jump table's leaf 0 on the current device (one small launch on
 // s, synchronous; the table sits in rs_jt_targets' code)
