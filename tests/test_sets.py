@@ -329,3 +329,29 @@ def test_sets_segments_off_the_bit_sliced_path(oracle, decode):
                 assert np.array_equal(got[g, oshift[g]:oshift[g] + stripes * k * ess], segs[g]), (k, ess, g)
         finally:
             c.close()
+
+
+def test_decode_sets_one_segment(oracle):
+    """One segment (its record passed in the prep launch's arguments) through
+    Decode: clean from k+3 shares, then with a corrupted piece, corrected in
+    place as infectious corrects share.Data."""
+    k, n, ess, stripes = 29, 80, 256, 50
+    rng = np.random.default_rng(1)
+    seg = rng.integers(0, 256, stripes * k * ess, dtype=np.uint8)
+    ref = oracle.FEC(k, n).encode_segment(seg, ess, threads=8)
+    st = [int(x) for x in rng.permutation(n)[:k + 3]]
+    c = Ctx(k, n, ess)
+    try:
+        d = torch.from_numpy(ref[None].copy()).cuda()
+        rc, outs = call_sets(c, d, [st], stripes, decode=True)
+        assert rc == 0, _native.strerror(rc)
+        assert np.array_equal(outs[0].cpu().numpy(), seg)
+        bad = ref[None].copy()
+        bad[0][st[2]] ^= 0x3C
+        d2 = torch.from_numpy(bad).cuda()
+        rc, outs = call_sets(c, d2, [st], stripes, decode=True)
+        assert rc == 0, _native.strerror(rc)
+        assert np.array_equal(outs[0].cpu().numpy(), seg)
+        assert np.array_equal(d2.cpu().numpy()[0], ref)
+    finally:
+        c.close()
