@@ -65,7 +65,8 @@ def random_sets(rng, k, n, count, extra=0):
     return [[int(x) for x in rng.permutation(n)[:k + extra]] for _ in range(count)]
 
 
-@pytest.mark.parametrize("k,n,stripes", [(29, 80, 41), (29, 80, 1), (20, 60, 130), (50, 80, 9), (4, 10, 257)])
+@pytest.mark.parametrize("k,n,stripes", [(29, 80, 41), (29, 80, 1), (20, 60, 130), (50, 80, 9), (4, 10, 257),
+                                          (1, 3, 20), (2, 4, 33)])
 def test_rebuild_sets_distinct_set_per_segment(oracle, k, n, stripes):
     """32 segments, 32 different share sets in one call: all parity (the most
     rows), all data present (no rows), seeded random 29-subsets (a mix of
