@@ -116,6 +116,28 @@ def main():
         host.append(time.perf_counter() - t0)
     torch.cuda.synchronize()
     res["batch"]["host_us_per_call_median"] = round(float(np.median(host)) * 1e6, 1)
+    # Decode with error detection over the same segments, each from a fresh set of k+4 clean shares
+    # (ec_decode_segments_sets: returns when done, so wall clock per call)
+    def dec_args(sets):
+        n = len(sets)
+        flat = [x for st_ in sets for x in st_]
+        return (n, (ctypes.c_int * n)(*[len(st_) for st_ in sets]), (ctypes.c_int * len(flat))(*flat),
+                (ctypes.c_void_p * len(flat))(*[pcs[g].data_ptr() + x * PLEN for g, st_ in enumerate(sets) for x in st_]),
+                (ctypes.c_void_p * n)(*[outs[g].data_ptr() for g in range(n)]))
+    dsets = [[[int(x) for x in rng.permutation(N)[:K + 4]] for _ in range(nseg)] for _ in range(args.reps)]
+    dargs = [dec_args(x) for x in dsets]
+    for a in dargs[:3]:
+        assert L.ec_decode_segments_sets(ctx, *a[:4], NSTRIPES, a[4], sptr) == 0
+    dw = []
+    for a in dargs:
+        t0 = time.perf_counter()
+        assert L.ec_decode_segments_sets(ctx, *a[:4], NSTRIPES, a[4], sptr) == 0
+        dw.append(time.perf_counter() - t0)
+    td = float(np.median(dw))
+    dalg = nseg * (PLEN * (K + 4) + SPAD)
+    res["decode_sets_k+4"] = {"segments_per_call": nseg, "wall_us_per_call_median": round(td * 1e6, 1),
+                              "us_per_segment": round(td / nseg * 1e6, 2), "frac": round(dalg / td / 1e9 / PEAK, 4),
+                              "note": "fresh seeded (k+4)-subsets, clean; bytes = the k+4 pieces read + the segment"}
     # the same 32 segments from ONE share set, warm plan, back to back on the stream: the
     # straight-line body and the jump-table body of ec_rebuild_segments_batched, timed as above
     one = all_sets[0][0]
