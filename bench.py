@@ -10,11 +10,13 @@ One step = every rank processes its whole shard once, in launches of
 `--batch` (default 32) segments, each launch pair being
   1. ec_encode_segments: 32 segments -> 80 pieces of 2,314,240 B each
      (segmentupload/encode.go:39-75 for all pieces at once);
-  2. ec_rebuild_segments_batched: the 32 segments rebuilt from exactly 29 of
-     their pieces (stripe.go:382-428 for all stripes at once).  The 29-piece
-     set cycles per launch through {51..79} (all parity, worst case) and seven
-     seeded random 29-subsets (default_rng(29)); decode plans are made in the
-     untimed warm-up.
+  2. ec_rebuild_segments_sets: the 32 segments rebuilt, each from exactly 29
+     of its pieces in a share set of its own -- the way uplink downloads: every
+     segment from whichever 29 pieces answered first (stripe.go:314-354), one
+     GetWithOptions per segment (client.go:273-308).  Every timed launch gets
+     32 fresh seeded 29-subsets (its first segment the all-parity {51..79},
+     the worst case); no decode plan is made or warmed (the decode rows are
+     solved on the GPU inside the call, rs_sets.hip).
 The segments are synthetic (device-generated random bytes, PadReader-padded to
 9040 stripes x 29 x 256 B), from a pool of 2 x 32 distinct segments per rank
 cycled over the shard: 1024 segments' pieces would not fit one GPU (SURVEY §8d
@@ -101,6 +103,13 @@ def share_sets():
     for _ in range(7):
         sets.append(sorted(rng.choice(N, K, replace=False).tolist()))
     return sets
+
+
+def fresh_launch_sets(seed: int, nb: int):
+    """The share sets of one timed decode launch: nb fresh seeded 29-subsets,
+    the first of them the all-parity {51..79} (worst case)."""
+    rng = np.random.default_rng(seed)
+    return [list(range(N - K, N))] + [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(nb - 1)]
 
 
 def cgroup_cpus():
@@ -513,6 +522,65 @@ def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 16):
             "note": "ec_rebuild_segments_sets; outside the timed region, informational, not in value"}
 
 
+def warm_shared_set_leg(L, ctx, encode, pieces, outs, segs, pool, B, dev, stream, sptr, rounds: int = 2):
+    """Informational, outside the timed region: the decode from ONE share set
+    per launch with its plan warm (ec_rebuild_segments_batched; the cycle of
+    {51..79} + 7 seeded random 29-subsets, each set's straight-line code made
+    and waited for first) -- what a caller that keeps reusing a set gets.
+    Timed as the headline decode: each decode launch right after an encode."""
+    sets = share_sets()
+    nums_c = [(ctypes.c_int * K)(*s) for s in sets]
+    ptrs_c = [[(ctypes.c_void_p * K)(*[p.data_ptr() + j * PIECE for j in s]) for s in sets] for p in pieces]
+
+    def dec(slot, i):
+        r = L.ec_rebuild_segments_batched(ctx, K, nums_c[i], ptrs_c[slot][i], NSTRIPES, B, N * PIECE, S_PAD,
+                                          outs[slot].data_ptr(), sptr)
+        if r:
+            raise RuntimeError(_native.strerror(r))
+    for slot in range(pool):
+        for i in range(len(sets)):
+            encode(slot, B)
+            dec(slot, i)
+    for st in sets:  # the sets' generated code, made in the background, ready before timing
+        L.ec_prepare_rebuild(ctx, K, (ctypes.c_int * K)(*st), 1)
+    t_settle = time.perf_counter()
+    j = 0
+    while time.perf_counter() - t_settle < 0.3:
+        encode(j % pool, B)
+        dec(j % pool, j % len(sets))
+        j += 1
+        torch.cuda.synchronize(dev)
+    ev = []
+    for r in range(rounds * len(sets)):
+        slot, i = r % pool, r % len(sets)
+        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        encode(slot, B)
+        e[0].record(stream)
+        dec(slot, i)
+        e[1].record(stream)
+        ev.append((e, i))
+    torch.cuda.synchronize(dev)
+    ok = True
+    for slot in range(pool):
+        outs[slot].zero_()
+        encode(slot, B)
+        dec(slot, slot % len(sets))
+        torch.cuda.synchronize(dev)
+        ok = ok and bool(torch.equal(outs[slot], segs[slot]))
+    per = [e[0].elapsed_time(e[1]) * 1e-3 for e, _ in ev]
+    t = sum(per) / len(per)
+    by_set = {}
+    for (e, i), x in zip(ev, per):
+        by_set.setdefault(i, []).append(x * 1e6 / B)
+    body = "straight-line" if L.ec_last_body(ctx) == _native.EC_BODY_STRAIGHT_LINE else "jump-table"
+    return {"kernel": f"rs_matmul_dma<NW, 1> ({body} body, LDS-DMA staging)", "avg_us": round(t * 1e6, 2),
+            "achieved_GBps": round(2 * S_PAD * B / t / 1e9, 1),
+            "frac": round(2 * S_PAD * B / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "us_per_segment_by_set": {f"set{i}:m={K - sum(1 for x in sets[i] if x < K)}": round(sum(v) / len(v), 2)
+                                      for i, v in sorted(by_set.items())},
+            "verified": ok, "note": "informational, not in value (uplink's downloads do not reuse sets)"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -557,20 +625,38 @@ def main():
     outs = [torch.empty((B, S_PAD), dtype=torch.uint8, device=dev) for _ in range(pool)]
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    sets = share_sets()
-    nums_c = [(ctypes.c_int * K)(*s) for s in sets]
-    ptrs_c = [[(ctypes.c_void_p * K)(*[p.data_ptr() + j * PIECE for j in s]) for s in sets] for p in pieces]
 
     def encode(slot, nb):
         r = L.ec_encode_segments(ctx, segs[slot].data_ptr(), nb, NSTRIPES, pieces[slot].data_ptr(), 0, sptr)
         if r:
             raise RuntimeError(_native.strerror(r))
 
-    def decode(slot, nb, i):
-        r = L.ec_rebuild_segments_batched(ctx, K, nums_c[i], ptrs_c[slot][i], NSTRIPES, nb, N * PIECE, S_PAD,
-                                          outs[slot].data_ptr(), sptr)
+    # the timed decode: a share set per segment, fresh every launch (ec_rebuild_segments_sets)
+    def set_args(slot, sets_):
+        """one call's arrays, made before the timed region (a Go caller holds its slices)"""
+        n = len(sets_)
+        flat = [x for st in sets_ for x in st]
+        return (n, (ctypes.c_int * n)(*[K] * n), (ctypes.c_int * len(flat))(*flat),
+                (ctypes.c_void_p * len(flat))(*[pieces[slot][g].data_ptr() + x * PIECE
+                                                for g, st in enumerate(sets_) for x in st]),
+                (ctypes.c_void_p * n)(*[outs[slot][g].data_ptr() for g in range(n)]), sets_)
+
+    def decode(slot, a):
+        n, nsh, nums, ptrs, optr, _ = a
+        r = L.ec_rebuild_segments_sets(ctx, n, nsh, nums, ptrs, NSTRIPES, optr, sptr)
         if r:
             raise RuntimeError(_native.strerror(r))
+
+    seed_base = 0x5E750000 + 1_000_003 * rank
+    launch_no = [0]
+
+    def fresh_args(slot, nb):
+        a = set_args(slot, fresh_launch_sets(seed_base + launch_no[0], nb))
+        launch_no[0] += 1
+        return a
+
+    def step_args():
+        return [fresh_args(b % pool, nb) for b, nb in enumerate(launches)]
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -579,13 +665,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    counter = [0]
-
-    def step(events=None):
+    def step(sargs, events=None):
         for b, nb in enumerate(launches):
             slot = b % pool
-            i = counter[0] % len(sets)
-            counter[0] += 1
             if events is not None:
                 # one marker per launch boundary: a launch pair starts at the previous pair's end
                 # marker (a marker costs the stream ~4 us), only the first is extra
@@ -597,49 +679,46 @@ def main():
                 e = (first, torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 encode(slot, nb)
                 e[1].record(stream)
-                decode(slot, nb, i)
+                decode(slot, sargs[b])
                 e[2].record(stream)
-                events.append((e, nb, i))
+                events.append((e, nb, sargs[b][5]))
             else:
                 encode(slot, nb)
-                decode(slot, nb, i)
+                decode(slot, sargs[b])
 
-    # warm-up: every share set once per pool slot (decode plans), the clock settle, then W steps
-    for slot in range(pool):
-        for i in range(len(sets)):
-            encode(slot, B)
-            decode(slot, B, i)
-    if hasattr(L, "ec_prepare_rebuild"):  # the sets' generated code, made in the background, ready before timing
-        for st in sets:
-            L.ec_prepare_rebuild(ctx, K, (ctypes.c_int * K)(*st), 1)
+    # every call's share sets and arrays, made before anything is timed (fresh per launch)
+    warm_args = [step_args() for _ in range(args.warmup)]
+    timed_args = [step_args() for _ in range(args.steps)]
+    cycle = [[fresh_args(slot, B) for _ in range(8)] for slot in range(pool)]
+    # warm-up: the clock settle (kernels loaded, share-set slots allocated), then W steps
     t_settle = time.perf_counter()
-    while time.perf_counter() - t_settle < args.settle_s:
-        for slot in range(pool):
-            encode(slot, B)
-            decode(slot, B, counter[0] % len(sets))
-            counter[0] += 1
-        torch.cuda.synchronize(dev)
-    for _ in range(args.warmup):
-        step()
+    i = 0
+    while time.perf_counter() - t_settle < args.settle_s or i < 2 * pool:
+        slot = i % pool
+        encode(slot, B)
+        decode(slot, cycle[slot][(i // pool) % 8])
+        i += 1
+        if i % (2 * pool) == 0:
+            torch.cuda.synchronize(dev)
+    for w in range(args.warmup):
+        step(warm_args[w])
     barrier()
 
     # timed: exactly K steps; per-launch HIP events on the launch stream (torch's current stream)
     events = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(events)
+    for st_ in range(args.steps):
+        step(timed_args[st_], events)
     barrier()
     wall = time.perf_counter() - t0
 
     seg_launched = sum(nb for _, nb, _ in events)
     t_enc = sum(e[0].elapsed_time(e[1]) for e, _, _ in events) * 1e-3  # s, all launches
     t_dec = sum(e[1].elapsed_time(e[2]) for e, _, _ in events) * 1e-3
-    full = [(e, i) for e, nb, i in events if nb == B]
+    full = [(e, st_) for e, nb, st_ in events if nb == B]
     t_enc_full = sum(e[0].elapsed_time(e[1]) for e, _ in full) / max(len(full), 1) * 1e-3  # s per B-launch
     t_dec_full = sum(e[1].elapsed_time(e[2]) for e, _ in full) / max(len(full), 1) * 1e-3
-    by_set = {}
-    for e, i in full:
-        by_set.setdefault(i, []).append(e[1].elapsed_time(e[2]) * 1e3 / B)
+    rows_timed = sorted(sum(1 for x in st if x >= K) for _, sets_ in full for st in sets_)
     # every rank's wall time (shard imbalance shows here) and a count of the ranks that took part
     rank_walls, ranks_seen = [round(wall, 6)], 1
     if use_dist:
@@ -652,19 +731,28 @@ def main():
         ranks_seen = int(seen.item())
         wall = max(rank_walls)
 
-    # correctness (outside the timed region): a full launch pair per pool slot rebuilds its input, and
-    # one segment's pieces match the oracle
+    # correctness (outside the timed region): every pool slot's segments encoded and rebuilt from
+    # fresh share sets (one segment all parity) equal their input, and one segment's pieces match
+    # the oracle
+    verified = True
     for slot in range(pool):
+        outs[slot].zero_()
         encode(slot, B)
-        decode(slot, B, slot % len(sets))
-    torch.cuda.synchronize(dev)
-    verified = all(bool(torch.equal(outs[sl], segs[sl])) for sl in range(pool))
+        decode(slot, fresh_args(slot, B))
+        torch.cuda.synchronize(dev)
+        verified = verified and bool(torch.equal(outs[slot], segs[slot]))
     verified = verified and oracle_spot_check(pieces[0][0], segs[0][0])
 
+    # informational, outside the timed region: the same decode from ONE warm share set per launch
+    # (ec_rebuild_segments_batched, the set's straight-line code made and waited for before
+    # timing) -- what a caller reusing a set gets; uplink's downloads do not (the timed leg)
+    warm = warm_shared_set_leg(L, ctx, encode, pieces, outs, segs, pool, B, dev, stream, sptr)
+
     # informational, outside the timed region: the parity-only encode (data pieces are the
-    # segment's own shares, served in place; the upload path of §8f row 1 uses this form).  Timed
-    # like the headline encode -- each launch followed by a rebuild, per-launch events -- and also
-    # back to back, where the denser VALU body runs at a lower sustained clock.
+    # segment's own shares, served in place; the upload path of §8f row 1 uses this form), and
+    # the encoder's own schedule without arithmetic (ec_encode_shape_probe, both forms).  Timed
+    # like the headline encode -- each launch followed by a decode launch, per-launch events --
+    # and also back to back, where a denser VALU body runs at a lower sustained clock.
     par = torch.empty((B, N - K, PIECE), dtype=torch.uint8, device=dev)
 
     def par_encode():
@@ -672,33 +760,53 @@ def main():
                                 sptr):
             raise RuntimeError("parity-only encode failed")
 
-    # the GPU idled through the checks above (oracle on the host): settle its clock again first, as
-    # before the timed steps, so the parity-only launches are timed in the same steady state
-    t_settle = time.perf_counter()
-    while time.perf_counter() - t_settle < max(args.settle_s, 0.1):
-        par_encode()
-        decode(1 % pool, B, counter[0] % len(sets))
-        counter[0] += 1
-        torch.cuda.synchronize(dev)
-    reps = 20
-    pev = []
-    for r in range(reps):
-        e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        e[0].record(stream)
-        par_encode()
-        e[1].record(stream)
-        decode(1 % pool, B, r % len(sets))
-        pev.append(e)
-    pe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    pe[0].record(stream)
-    for _ in range(reps):
-        par_encode()
-    pe[1].record(stream)
-    pe[1].synchronize()
-    t_par = sum(a.elapsed_time(b) for a, b in pev) / reps * 1e-3
-    t_par_b2b = pe[0].elapsed_time(pe[1]) / reps * 1e-3
+    def shape_full():  # (writes pieces[0] with copies, not parity: re-encoded after)
+        if L.ec_encode_shape_probe(ctx, segs[0].data_ptr(), B, NSTRIPES, pieces[0].data_ptr(), 0, sptr):
+            raise RuntimeError("ec_encode_shape_probe failed")
+
+    def shape_par():
+        if L.ec_encode_shape_probe(ctx, segs[0].data_ptr(), B, NSTRIPES, par.data_ptr(), _native.EC_FLAG_PARITY_ONLY,
+                                   sptr):
+            raise RuntimeError("ec_encode_shape_probe (parity only) failed")
+
+    def timed_like_headline(launch, reps=20):
+        """(alternating with a decode launch, as timed; back to back) seconds per launch"""
+        # the GPU idled through the checks above (oracle on the host): settle its clock again first,
+        # as before the timed steps, so the launches are timed in the same steady state
+        t_settle = time.perf_counter()
+        j = 0
+        while time.perf_counter() - t_settle < max(args.settle_s, 0.1):
+            launch()
+            decode(1 % pool, cycle[1 % pool][j % 8])
+            j += 1
+            torch.cuda.synchronize(dev)
+        pev = []
+        for r in range(reps):
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record(stream)
+            launch()
+            e[1].record(stream)
+            decode(1 % pool, cycle[1 % pool][r % 8])
+            pev.append(e)
+        pe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        pe[0].record(stream)
+        for _ in range(reps):
+            launch()
+        pe[1].record(stream)
+        pe[1].synchronize()
+        return (sum(a.elapsed_time(b) for a, b in pev) / reps * 1e-3, pe[0].elapsed_time(pe[1]) / reps * 1e-3)
+
+    t_par, t_par_b2b = timed_like_headline(par_encode)
     encode(0, B)
+    torch.cuda.synchronize(dev)
     verified = verified and bool(torch.equal(par, pieces[0][:, K:]))
+    shape_ok = hasattr(L, "ec_encode_shape_probe")
+    t_shape = t_shape_b2b = t_shape_par = t_shape_par_b2b = None
+    if shape_ok:
+        t_shape, t_shape_b2b = timed_like_headline(shape_full)
+        t_shape_par, t_shape_par_b2b = timed_like_headline(shape_par)
+        encode(0, B)  # (pieces[0] holds the probe's copies: the real pieces again)
+        torch.cuda.synchronize(dev)
     del par
     if use_dist:
         import torch.distributed as dist
@@ -717,14 +825,13 @@ def main():
         "encode": {"kernel": (f"{ENC_FULL_KERNEL} (special)" if enc_name == "special"
                               else f"rs_matmul_dma<7, 1> ({enc_name})"), "avg_us": round(t_enc_full * 1e6, 2),
                    "bytes_per_launch": int(enc_bytes), "achieved_GBps": round(enc_gbps, 1)},
-        "decode": {"kernel": ("rs_matmul_dma<NW, 1> (straight-line body, LDS-DMA staging)"
-                              if L.ec_last_body(ctx) == _native.EC_BODY_STRAIGHT_LINE
-                              else "rs_matmul_jt<NW, false> (jump-table body)"),
+        "decode": {"kernel": "rs_sets_prep + rs_matmul_sets<NW> (a share set per segment, decode rows solved on "
+                             "the GPU, jump-table body, LDS-DMA staging)",
                    "avg_us": round(t_dec_full * 1e6, 2),
                    "bytes_per_launch": int(dec_bytes), "achieved_GBps": round(dec_gbps, 1),
-                   "us_per_segment_by_set": {
-                       f"set{i}:m={K - sum(1 for x in sets[i] if x < K)}": round(sum(v) / len(v), 2)
-                       for i, v in sorted(by_set.items())}},
+                   "rows_per_segment": (f"{rows_timed[0]}..{rows_timed[-1]} (median {rows_timed[len(rows_timed) // 2]})"
+                                        if rows_timed else None)},
+        "decode_warm_shared_set": warm,
     }
     par_bytes = B * S_PAD * (1 + (N - K) / K)
     par_frac = round(par_bytes / t_par / 1e9 / HBM_PEAK_GBPS, 4)
@@ -734,6 +841,19 @@ def main():
         "avg_us_back_to_back": round(t_par_b2b * 1e6, 2),
         "bytes_per_launch": int(par_bytes), "achieved_GBps": round(par_bytes / t_par / 1e9, 1),
         "frac": par_frac, "note": "informational, not in value"}
+    shape_gbps = enc_bytes / t_shape / 1e9 if t_shape else None
+    shape_par_gbps = par_bytes / t_shape_par / 1e9 if t_shape_par else None
+    if shape_ok:
+        kernels["encode_shape_probe"] = {
+            "kernel": "rs_encode_shape<29, 80, 8, 4, true/false> (ec_encode_shape_probe: the encoder's body "
+                      "without its multiply-accumulate)",
+            "full_avg_us": round(t_shape * 1e6, 2), "full_avg_us_back_to_back": round(t_shape_b2b * 1e6, 2),
+            "full_GBps": round(shape_gbps, 1),
+            "parity_only_avg_us": round(t_shape_par * 1e6, 2),
+            "parity_only_avg_us_back_to_back": round(t_shape_par_b2b * 1e6, 2),
+            "parity_only_GBps": round(shape_par_gbps, 1),
+            "note": "same loaders, LDS ring, tile queue, slicing and stores as the encoder, no GF arithmetic; "
+                    "timed like the headline encode (each launch followed by a decode launch) and back to back"}
     # SURVEY §8d, VERDICT r4 item 4: on-box ceilings next to the spec peak -- the library's own
     # streaming kernels (ec_bw_probe, no arithmetic) in the read:write mixes of the kernels measured
     # here, in the best shapes of the round-2 probes; outside the timed region
@@ -773,7 +893,8 @@ def main():
                                "(BASELINE configs[3], each segment as configs[1]+[2])",
                    "k": K, "n": N, "erasure_share_size": ESS, "total_segments_per_step": args.total_segments,
                    "segments_this_rank": count, "segments_per_launch": B, "stripes_per_segment": NSTRIPES,
-                   "decode_share_sets": "cycle of {51..79} + 7 seeded random 29-subsets",
+                   "decode_share_sets": "a fresh seeded 29-subset per segment and launch (each launch's first "
+                                        "segment {51..79}); no plan made or warmed",
                    "parallelism": f"segments sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(dk["achieved_GBps"], 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4),
@@ -785,9 +906,16 @@ def main():
                      "frac_of_mix": _ratio(enc_gbps, ceil.get("encode_mix")),
                      "frac_of_mix_parity_only": _ratio(par_bytes / t_par / 1e9, ceil.get("parity_mix")),
                      "frac_decode_of_copy": _ratio(dec_gbps, ceil.get("copy")),
+                     "encode_shape_GBps_on_box": _r(shape_gbps, 1),
+                     "parity_shape_GBps_on_box": _r(shape_par_gbps, 1),
+                     "frac_of_shape": _ratio(enc_gbps, shape_gbps),
+                     "frac_of_shape_parity_only": _ratio(par_bytes / t_par / 1e9, shape_par_gbps),
+                     "shape_frac_of_peak": _ratio(shape_gbps, HBM_PEAK_GBPS),
                      "ceilings_note": "ec_bw_probe: one-shot grid, each wave R KiB in / W KiB out, 16 B per lane, "
                                       "non-temporal, no arithmetic; copy 1:1, encode mix 4:11 (the encode's 29:80), "
-                                      "parity mix 4:7 (29:51); 1 GiB read, median of 10 launches"},
+                                      "parity mix 4:7 (29:51); 1 GiB read, median of 10 launches; encode shape: "
+                                      "the encoder's own schedule without arithmetic (ec_encode_shape_probe), timed "
+                                      "as the encode is"},
         "kernels": kernels,
         "encode_gibps": round(B * S_PAD / 2**30 / t_enc_full, 2),
         "decode_gibps": round(B * S_PAD / 2**30 / t_dec_full, 2),

@@ -238,6 +238,12 @@ int ec_upload_hashes(ec_upload *u, uint8_t *hashes);
 int ec_upload_end(ec_upload *u);
 void *ec_host_alloc(size_t bytes); /* pinned (hipHostMalloc); NULL on failure */
 void ec_host_free(void *p);
+/* Device memory on the current device for the device-pointer calls (the
+ * share-set calls' pieces and outputs; a Go binding has no other allocator),
+ * and a synchronous copy between any two of host / pinned / device memory. */
+void *ec_device_alloc(size_t bytes); /* hipMalloc; NULL on failure */
+void ec_device_free(void *p);
+int ec_copy(void *dst, const void *src, size_t bytes); /* hipMemcpy(hipMemcpyDefault) */
 
 /* ---- BLAKE3-256 piece hashes (github.com/zeebo/blake3 v0.2.3, go.mod:29) ----
  * Replace the per-piece hash.Hash fed by io.TeeReader during upload
@@ -311,6 +317,15 @@ int ec_gcm_open_host(const uint8_t key[32], const uint8_t nonce[12], const uint8
 #define EC_PROBE_ENCODE_MIX 1 /* 4 : 11    (the full encode's 29 : 80) */
 #define EC_PROBE_PARITY_MIX 2 /* 4 : 7     (the parity-only encode's 29 : 51) */
 int ec_bw_probe(int shape, const uint8_t *src, size_t read_bytes, uint8_t *dst, size_t *moved, ec_stream stream);
+/* The RS(29,80) encoder's own memory schedule without its arithmetic: exactly
+ * ec_encode_segments' launch (same loaders, LDS ring, tile queue, slicing,
+ * copy-through and parity stores, flags as there), with the GF
+ * multiply-accumulate removed -- each parity row stored is a copy of the
+ * tile's last input share, so the pieces written are NOT the code's.  The
+ * on-box ceiling of the encoder's access pattern (bench.py); measurement only.
+ * EC_ERR_UNSUPPORTED for any other (k, n), or ess / pointers not 16-aligned. */
+int ec_encode_shape_probe(const ec_ctx *ctx, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                          int flags, ec_stream stream);
 
 /* ---- device helpers ---- */
 int ec_device_count(void);

@@ -168,6 +168,96 @@ static void scheme_surface(int k, int n, int ess, int body) {
     ec_destroy(ctx);
 }
 
+/* A share set per segment (the cgo entry for concurrent downloads,
+ * INTEGRATION.md "Many downloads at once"): nseg segments in device memory,
+ * each rebuilt from its own set by ec_rebuild_segments_sets, then decoded with
+ * error detection by ec_decode_segments_sets from k + 2 shares with one piece
+ * corrupted -- outputs against the input, pieces against the oracle's. */
+static void share_sets_surface(int k, int n, int ess) {
+    ec_ctx *ctx = NULL;
+    int rc = ec_create(k, n, ess, &ctx);
+    CHECK(rc == EC_OK, "ec_create(%d,%d,%d) = %d", k, n, ess, rc);
+    if (rc) return;
+    uint8_t *enc = malloc((size_t)n * k), *vand = malloc((size_t)n * k);
+    or_new_fec(k, n, enc, vand);
+    enum { NSEG = 3 };
+    const size_t stripes = 37, stripe = (size_t)k * ess, spad = stripes * stripe, plen = stripes * (size_t)ess;
+    uint8_t *segs = malloc(NSEG * spad), *pieces = malloc(NSEG * (size_t)n * plen), *back = malloc(NSEG * spad);
+    fill(segs, NSEG * spad);
+    for (size_t g = 0; g < NSEG; g++)
+        or_baseline_encode_segment(k, n, ess, enc, segs + g * spad, stripes, pieces + g * (size_t)n * plen, 1);
+    uint8_t *d_pieces = ec_device_alloc(NSEG * (size_t)n * plen), *d_out = ec_device_alloc(NSEG * spad);
+    CHECK(d_pieces && d_out, "ec_device_alloc");
+    if (!d_pieces || !d_out) goto done;
+    CHECK(ec_copy(d_pieces, pieces, NSEG * (size_t)n * plen) == EC_OK, "ec_copy H2D");
+    /* segment 0: the last k shares (all parity when n >= 2k); 1: every other share from the top,
+     * shuffled; 2: the data shares but one, plus share n-1 */
+    int ns[NSEG], nums[NSEG * 256];
+    const uint8_t *ptrs[NSEG * 256];
+    uint8_t *outs[NSEG];
+    int at = 0;
+    for (int g = 0; g < NSEG; g++) {
+        ns[g] = k;
+        for (int i = 0; i < k; i++) {
+            int num = g == 0 ? n - k + i : g == 1 ? (n - 1 - 2 * i + n) % n : (i < k - 1 ? i : n - 1);
+            if (g == 1 && 2 * k > n) num = n - 1 - i;
+            nums[at + i] = num;
+        }
+        if (g == 1)
+            for (int i = k - 1; i > 0; i--) { /* any order */
+                const int j = rnd8() % (i + 1), t = nums[at + i];
+                nums[at + i] = nums[at + j], nums[at + j] = t;
+            }
+        for (int i = 0; i < k; i++) ptrs[at + i] = d_pieces + ((size_t)g * n + nums[at + i]) * plen;
+        outs[g] = d_out + g * spad;
+        at += k;
+    }
+    printf("[%9.1f ms]   ec_rebuild_segments_sets RS(%d,%d)\n", ms(), k, n);
+    rc = ec_rebuild_segments_sets(ctx, NSEG, ns, nums, ptrs, stripes, outs, NULL);
+    CHECK(rc == EC_OK, "ec_rebuild_segments_sets rc %d (%s)", rc, ec_strerror(rc));
+    CHECK(ec_copy(back, d_out, NSEG * spad) == EC_OK, "ec_copy D2H");
+    for (int g = 0; g < NSEG; g++)
+        CHECK(memcmp(back + g * spad, segs + g * spad, spad) == 0, "sets rebuild: segment %d != input (%d,%d)", g, k, n);
+    if (n - k >= 2) {
+        /* Decode: k + 2 shares per segment, segment 1's second share corrupted in one byte */
+        uint8_t *dptr[NSEG * 256];
+        at = 0;
+        for (int g = 0; g < NSEG; g++) {
+            ns[g] = k + 2;
+            for (int i = 0; i < k + 2; i++) {
+                nums[at + i] = (g + 7 * i) % n; /* (7 is prime to every n here) */
+                dptr[at + i] = d_pieces + ((size_t)g * n + nums[at + i]) * plen;
+            }
+            at += k + 2;
+        }
+        uint8_t *bad = dptr[(k + 2) + 1] + plen / 2 + 5, flip;
+        CHECK(ec_copy(&flip, bad, 1) == EC_OK, "read a byte");
+        flip ^= 0xA5;
+        CHECK(ec_copy(bad, &flip, 1) == EC_OK, "corrupt a byte");
+        uint8_t *zero = calloc(NSEG * spad, 1);
+        CHECK(ec_copy(d_out, zero, NSEG * spad) == EC_OK, "clear outputs");
+        free(zero);
+        printf("[%9.1f ms]   ec_decode_segments_sets RS(%d,%d)\n", ms(), k, n);
+        rc = ec_decode_segments_sets(ctx, NSEG, ns, nums, dptr, stripes, outs, NULL);
+        CHECK(rc == EC_OK, "ec_decode_segments_sets rc %d (%s)", rc, ec_strerror(rc));
+        CHECK(ec_copy(back, d_out, NSEG * spad) == EC_OK, "ec_copy D2H");
+        for (int g = 0; g < NSEG; g++)
+            CHECK(memcmp(back + g * spad, segs + g * spad, spad) == 0, "sets decode: segment %d != input (%d,%d)", g, k,
+                  n);
+        /* the corrupted share is corrected in place, as infectious corrects share.Data */
+        uint8_t *fixed = malloc(plen);
+        CHECK(ec_copy(fixed, dptr[(k + 2) + 1], plen) == EC_OK, "ec_copy D2H");
+        CHECK(memcmp(fixed, pieces + ((size_t)n + nums[(k + 2) + 1]) * plen, plen) == 0,
+              "sets decode: corrupted piece not corrected (%d,%d)", k, n);
+        free(fixed);
+    }
+done:
+    ec_device_free(d_pieces);
+    ec_device_free(d_out);
+    free(segs), free(pieces), free(back), free(enc), free(vand);
+    ec_destroy(ctx);
+}
+
 /* BLAKE3 piece hashes and AES-256-GCM blocks through the host entry points */
 static void adjacent_stages(void) {
     const size_t lens[] = {0, 1, 1024, 1025, 300000};
@@ -221,6 +311,11 @@ int main(int argc, char **argv) {
             printf("[%9.1f ms] RS(%d,%d) ess %d body %d\n", ms(), cfg[i][0], cfg[i][1], cfg[i][2], body);
             scheme_surface(cfg[i][0], cfg[i][1], cfg[i][2], body);
         }
+    }
+    const int scfg[][3] = {{29, 80, 256}, {4, 10, 256}, {20, 60, 4096}};
+    for (size_t i = 0; i < sizeof scfg / sizeof scfg[0]; i++) {
+        printf("[%9.1f ms] share sets RS(%d,%d) ess %d\n", ms(), scfg[i][0], scfg[i][1], scfg[i][2]);
+        share_sets_surface(scfg[i][0], scfg[i][1], scfg[i][2]);
     }
     printf("[%9.1f ms] adjacent stages\n", ms());
     adjacent_stages();

@@ -25,8 +25,7 @@ int main(int argc, char **argv) {
     }
     uint8_t *seg = malloc((size_t)k * ess * stripes), *pieces = malloc((size_t)n * ess * stripes);
     for (size_t i = 0; i < (size_t)k * ess * stripes; i++) seg[i] = (uint8_t)(i * 131 + 7);
-    /* the first whole-segment encode of this (k, n) starts the compile and runs on the
-     * runtime-matrix kernel meanwhile */
+    /* a small encode (8 tiles) runs on the runtime-matrix kernel and starts no compile */
     rc = ec_encode_segments_host(ctx, seg, 1, stripes, pieces, 0);
     if (rc != EC_OK) {
         fprintf(stderr, "ec_encode_segments_host: %s\n", ec_strerror(rc));
@@ -36,7 +35,8 @@ int main(int argc, char **argv) {
         fprintf(stderr, "piece 0 is not the first share of each stripe\n");
         return 4;
     }
-    /* 0 = the compiled encoder is not loaded yet: the compile is still running */
+    /* ec_prepare_encoder without wait starts the compile; 0 = the compiled encoder is not
+     * loaded yet: the compile is still running */
     if (ec_prepare_encoder(ctx, 0) != 0) {
         fprintf(stderr, "RS(%d,%d)'s encoder was already compiled: the test needs an empty cache\n", k, n);
         return 5;

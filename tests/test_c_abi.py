@@ -18,16 +18,18 @@ def test_c_client_links_against_the_library():
     assert "libuplink_ec.so" in out and "not found" not in out
 
 
-def _run_client(binary, timeout=120):
-    """Run a C client with the library's diagnostic log on (UPLINK_EC_LOG: every
-    run-time compile and module load with its duration) and run-time encoder
-    compilation off (UPLINK_EC_JIT=0): its RS(10,20) per-stripe encodes would
-    start a hiprtc compile that process exit then waits for, minutes when the
-    box's disk cache is cold -- the checked client's round-2 and round-4
-    timeouts; the compile path has its own tests (exit_test).
-    On a timeout, fail with everything it printed so far: the client stamps
-    each phase, so the last line names where it stopped."""
-    env = dict(os.environ, UPLINK_EC_LOG="1", UPLINK_EC_JIT="0")
+def _run_client(binary, cache_dir, timeout=120):
+    """Run a C client in the environment an integrator gets by default --
+    run-time encoder compilation on, an empty disk cache -- with the library's
+    diagnostic log on (UPLINK_EC_LOG: every run-time compile and module load
+    with its duration).  Its RS(10,20) per-stripe calls must not start a hiprtc
+    compile (the library starts one only for whole-segment launches), so the
+    process exits in seconds instead of waiting for one at exit (the checked
+    client's round-2, round-4 and round-5 timeouts).  On a
+    timeout, fail with everything it printed so far: the client stamps each
+    phase, so the last line names where it stopped."""
+    env = dict(os.environ, UPLINK_EC_LOG="1", UPLINK_EC_JIT_CACHE=str(cache_dir))
+    env.pop("UPLINK_EC_JIT", None)
     try:
         return subprocess.run([binary], capture_output=True, text=True, timeout=timeout, env=env)
     except subprocess.TimeoutExpired as e:
@@ -36,16 +38,22 @@ def _run_client(binary, timeout=120):
         pytest.fail(f"{os.path.basename(binary)} timed out after {timeout} s; its output:\n{out}\n{err}")
 
 
+def _no_compile_started(r):
+    log = r.stdout + r.stderr
+    assert "encoder: start" not in log and "joining 1 encoder compile" not in log, log
+
+
 @pytest.mark.gpu
-def test_c_client_on_gpu():
+def test_c_client_on_gpu(tmp_path):
     assert os.path.exists(BIN), "tests/c/build/abi_test missing: build() compiles it"
-    r = _run_client(BIN)
+    r = _run_client(BIN, tmp_path / "jit")
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().splitlines()[-1].startswith("ok")
+    _no_compile_started(r)
 
 
 @pytest.mark.gpu
-def test_c_client_on_gpu_checked_library():
+def test_c_client_on_gpu_checked_library(tmp_path):
     """The same client against libuplink_ec_checked.so, whose stripe kernels
     compare every global address with the launch's declared byte ranges and
     trap (with the site printed) on one outside them.  First, before any GPU
@@ -55,10 +63,11 @@ def test_c_client_on_gpu_checked_library():
     ids = [subprocess.run([b, "--build-id"], capture_output=True, text=True, timeout=30).stdout.strip()
            for b in (BIN, BIN_CHECKED)]
     assert ids[0] and ids[0] == ids[1], f"checked library build {ids[1]} is not the product's {ids[0]}: rebuild both"
-    r = _run_client(BIN_CHECKED)
+    r = _run_client(BIN_CHECKED, tmp_path / "jit")
     assert "uplink_ec checked" not in r.stdout + r.stderr, r.stdout + r.stderr
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().splitlines()[-1].startswith("ok")
+    _no_compile_started(r)
 
 
 BIN_EXIT = os.path.join(HERE, "c", "build", "exit_test")

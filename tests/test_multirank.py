@@ -107,6 +107,11 @@ def test_bench_two_ranks_hip_path_gloo_on_one_gpu():
     fs = line["fresh_share_sets"]
     assert fs["32 segments, 32 fresh seeded 29-subsets per launch"]["verified"] is True
     assert fs["one segment, fresh set"]["wall_us_median"] > 0
+    # the timed decode is the share-set pass (fresh sets), the warm shared-set
+    # decode and the encoder's no-arithmetic schedule are reported beside it
+    assert line["kernels"]["decode"]["kernel"].startswith("rs_sets_prep")
+    assert line["kernels"]["decode_warm_shared_set"]["verified"] is True
+    assert line["roofline"]["encode_shape_GBps_on_box"] > 0 and line["roofline"]["frac_of_shape"] > 0
 
 
 @pytest.mark.gpu

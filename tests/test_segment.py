@@ -329,3 +329,21 @@ def test_upload_end_waits_for_callers_inside():
         assert all(r in (0, 1, NAT.EC_ERR_INVALID_ARG) for r in rcs), rcs
     seg.close()
     pieces.close()
+
+
+def test_reader_used_after_close_allocates_nothing():
+    """piece_reader / piece_hash after close() raise before
+    any buffer is taken from the pool or any upload is begun (the buffers went
+    back to the pool at close; a new upload would be reclaimed only by
+    __del__)."""
+    rs = _rs(29, 80, 256)
+    data = np.random.default_rng(5).integers(0, 256, 100000, dtype=np.uint8).tobytes()
+    for touch_first in (False, True):
+        spr = segment.SegmentPieceReader(data, rs, hash_pieces=True)
+        if touch_first:
+            spr.piece_reader(30).read()
+        spr.close()
+        for call in (lambda: spr.piece_reader(1), lambda: spr.piece_reader(40), lambda: spr.piece_hash(2)):
+            with pytest.raises(eestream.EEStreamError, match="after close"):
+                call()
+            assert spr._upload is None and spr._bufs == [] and spr._padded is None

@@ -129,14 +129,19 @@ def main():
     for a in dargs[:3]:
         assert L.ec_decode_segments_sets(ctx, *a[:4], NSTRIPES, a[4], sptr) == 0
     dw = []
+    dec_ok = True
     for a in dargs:
+        outs.zero_()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         assert L.ec_decode_segments_sets(ctx, *a[:4], NSTRIPES, a[4], sptr) == 0
         dw.append(time.perf_counter() - t0)
+        dec_ok = dec_ok and bool(torch.equal(outs[:nseg], segs[:nseg]))  # (after the timed call)
     td = float(np.median(dw))
     dalg = nseg * (PLEN * (K + 4) + SPAD)
     res["decode_sets_k+4"] = {"segments_per_call": nseg, "wall_us_per_call_median": round(td * 1e6, 1),
                               "us_per_segment": round(td / nseg * 1e6, 2), "frac": round(dalg / td / 1e9 / PEAK, 4),
+                              "verified": dec_ok,
                               "note": "fresh seeded (k+4)-subsets, clean; bytes = the k+4 pieces read + the segment"}
     # the same 32 segments from ONE share set, warm plan, back to back on the stream: the
     # straight-line body and the jump-table body of ec_rebuild_segments_batched, timed as above

@@ -103,7 +103,11 @@ SIGNATURES = {
     "ec_upload_end": (ctypes.c_int, [vp]),
     "ec_host_alloc": (vp, [ctypes.c_size_t]),
     "ec_host_free": (None, [vp]),
+    "ec_device_alloc": (vp, [ctypes.c_size_t]),
+    "ec_device_free": (None, [vp]),
+    "ec_copy": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
     "ec_bw_probe": (ctypes.c_int, [ctypes.c_int, vp, ctypes.c_size_t, vp, ctypes.POINTER(ctypes.c_size_t), vp]),
+    "ec_encode_shape_probe": (ctypes.c_int, [vp, vp, ctypes.c_size_t, ctypes.c_size_t, vp, ctypes.c_int, vp]),
     "ec_device_count": (ctypes.c_int, []),
     "ec_set_device": (ctypes.c_int, [ctypes.c_int]),
     "ec_encode_kernel_name": (ctypes.c_char_p, [vp]),

@@ -700,7 +700,7 @@ const char *ec_encode_kernel_name(const ec_ctx *c) {
     if (c->n == c->k) return "copy";
     if (sl_encoder(c)) return "straight-line";
     DeviceGuard dg(c->device);
-    const EncoderKernel *e = find_encoder(c->k, c->n);
+    const EncoderKernel *e = find_encoder(c->k, c->n, false, false);  // (a query: starts no compile)
     return e ? (e->jit ? "special-jit" : "special") : "generic";
 }
 
@@ -719,7 +719,7 @@ int ec_prepare_encoder(const ec_ctx *c, int wait) {
 namespace uplink_ec {
 namespace capi {
 int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, size_t s0, size_t s1,
-                        uint8_t *pieces, int flags, hipStream_t s) {
+                        uint8_t *pieces, int flags, hipStream_t s, bool shape_probe) {
     if (!c || !segs || !pieces) return EC_ERR_INVALID_ARG;
     if (nseg == 0 || s1 <= s0) return EC_OK;
     const int k = c->k, n = c->n, ess = c->ess;
@@ -746,13 +746,18 @@ int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, s
     for (int r = 0; r < std::min(n - k, kMaxOps); r++) a.out_off[r] = out_off[r];
     fill_geometry(a, ess, (int64_t)(s1 - s0), (int64_t)nseg);
     const bool bits = (ess % 16) == 0 && aligned16(segs) && aligned16(pieces);
+    if (shape_probe && (!bits || !shape_probe_encoder(k, n))) return EC_ERR_UNSUPPORTED;
     if (n == k) {  // replication of the data only: copies, no parity rows
         if (parity_only) return EC_OK;
     } else if (bits) {
         // few parity rows: the runtime-matrix kernel with the parity plan's
         // straight-line code (run_matmul picks it for launches this large)
         const bool sl = sl_encoder(c) && (c->body == EC_BODY_STRAIGHT_LINE || a.total_tiles >= kSlMinTiles);
-        const EncoderKernel *ek = sl ? nullptr : find_encoder(c->k, c->n);
+        // (a run-time compile of this code's encoder is started only by launches
+        // large enough to pay for it: never by per-stripe or few-stripe work)
+        const EncoderKernel *ek = shape_probe ? shape_probe_encoder(k, n)
+                                  : sl        ? nullptr
+                                              : find_encoder(c->k, c->n, false, a.total_tiles >= kJitMinTiles);
         if (ek) {
             a.coef = nullptr;
             set_extents(a, (int64_t)nseg, c->d_chk);
@@ -781,6 +786,14 @@ int ec_encode_segments(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_
     DeviceGuard dg(cc->device);
     return encode_range(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, 0, nstripes, pieces, flags,
                         (hipStream_t)stream);
+}
+
+int ec_encode_shape_probe(const ec_ctx *cc, const uint8_t *segs, size_t nseg, size_t nstripes, uint8_t *pieces,
+                          int flags, ec_stream stream) {
+    if (!cc) return EC_ERR_INVALID_ARG;
+    DeviceGuard dg(cc->device);
+    return encode_range(const_cast<ec_ctx *>(cc), segs, nseg, nstripes, 0, nstripes, pieces, flags,
+                        (hipStream_t)stream, true);
 }
 
 int ec_rebuild_segments(const ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces,
@@ -893,7 +906,7 @@ static int single_batch_once(ec_ctx *c, SingleReq *const *req, size_t nreq, size
             for (int r = 0; r < std::min(n - k, kMaxOps); r++) a.out_off[r] = out_off[r];
             fill_geometry(a, (int)bs, (int64_t)nreq, 1);
             const bool bits = bs % 16 == 0;
-            const EncoderKernel *ek = bits ? find_encoder(k, n) : nullptr;
+            const EncoderKernel *ek = bits ? find_encoder(k, n, false, false) : nullptr;  // (starts no compile)
             if (ek) {
                 set_extents(a, 1, c->d_chk);
                 if (launch_encode_special(*ek, a, 0, st) != hipSuccess) {
@@ -1086,6 +1099,22 @@ void *ec_host_alloc(size_t bytes) {
 
 void ec_host_free(void *p) {
     if (p) (void)hipHostFree(p);
+}
+
+void *ec_device_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+    return p;
+}
+
+void ec_device_free(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+int ec_copy(void *dst, const void *src, size_t bytes) {
+    if (!bytes) return EC_OK;
+    if (!dst || !src) return EC_ERR_INVALID_ARG;
+    return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess ? EC_OK : EC_ERR_DEVICE;
 }
 
 // Segment g goes through slot g % 3: H2D on that slot's stream, then the

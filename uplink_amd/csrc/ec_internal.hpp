@@ -300,9 +300,13 @@ struct SetsSlot {
     size_t tgt_cap = 0;
     uint32_t *d_words = nullptr;  // device: [0] done counter, [1 + g] segment g's syndrome count (stage_cap + 1)
     uint32_t *h_words = nullptr;  // pinned: [0] done sequence number, [1 + g] syndrome counts read back (Decode)
+    size_t words_cap = 0;         // entries of h_words
     uint32_t seq = 0;             // of the slot's latest call
     bool busy = false;            // a caller is filling or launching it
-    bool dead = false;            // a launch failed after the prep: never reused
+    bool dead = false;            // a launch failed after the prep and the device did not recover: never reused
+    // buffers a slot outgrew: freed with the slot (ec_destroy), never on the call
+    // path, where hipFree / hipHostFree would synchronise the whole device
+    std::vector<void *> old_dev, old_host;
     ~SetsSlot() {
         if (h_stage) (void)hipHostFree(h_stage);
         if (d_stage) (void)hipFree(d_stage);
@@ -310,12 +314,21 @@ struct SetsSlot {
         if (d_tgt) (void)hipFree(d_tgt);
         if (d_words) (void)hipFree(d_words);
         if (h_words) (void)hipHostFree(h_words);
+        for (void *p : old_dev) (void)hipFree(p);
+        for (void *p : old_host) (void)hipHostFree(p);
     }
     bool idle() const { return !busy && !dead && __atomic_load_n(h_words, __ATOMIC_ACQUIRE) == seq; }
 };
 
 struct SetsRing {
-    static constexpr size_t kMaxSlots = 16;  // calls in flight per context before a caller waits
+    static constexpr size_t kMaxSlots = 16;  // live calls in flight per context before a caller waits
+    // segments and leaf-table words a new slot is sized for (a pass of sets_export,
+    // kPass segments of up to 128 inputs): a slot grows -- geometrically -- only for
+    // larger ec_rebuild_segments_batched calls
+    static constexpr size_t kInitSegs = 64, kInitTgtWords = (size_t)64 * 1024;
+    // a caller waits at most this long for a slot (calls in flight that never
+    // complete, e.g. a stream whose work never runs): then EC_ERR_DEVICE
+    static constexpr int kAcquireTimeoutMs = 30000;
     std::mutex mu;
     std::vector<std::unique_ptr<SetsSlot>> slots;
 };
@@ -426,6 +439,11 @@ namespace capi {
 // EC_BODY_AUTO: its module costs a code generation and a module load once per
 // plan, which only pays over many stripes.
 constexpr int64_t kSlMinTiles = 64;
+// Launches of at least this many tiles start the run-time compilation of their
+// code's encoder when the library has none built in (rs_encoder_registry.cpp):
+// a compile takes seconds of host CPU, per-stripe calls (1 tile) never start
+// one, and a process that started one waits for it at exit.
+constexpr int64_t kJitMinTiles = 256;
 
 // ec_capi.cpp
 int hip_fail(hipError_t e);
@@ -442,8 +460,9 @@ int rebuild_with_plan(ec_ctx *c, MatPlan &plan, const std::vector<int> &order, c
                       int64_t out_seg_stride, uint8_t *out, hipStream_t s);
 int rebuild_device(ec_ctx *c, int nshares, const int *nums, const uint8_t *const *pieces, int ess, int64_t nstripes,
                    int64_t nseg, int64_t piece_seg_stride, int64_t out_seg_stride, uint8_t *out, hipStream_t s);
+// shape_probe: run the encoder's no-arithmetic form instead (ec_encode_shape_probe)
 int encode_range(ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes, size_t s0, size_t s1,
-                 uint8_t *pieces, int flags, hipStream_t s);
+                 uint8_t *pieces, int flags, hipStream_t s, bool shape_probe = false);
 size_t align_up(size_t x, size_t a);
 B3View data_view(const ec_ctx *c, const uint8_t *segs, size_t nseg, size_t nstripes);
 B3View parity_view(const ec_ctx *c, const uint8_t *parity, size_t nseg, size_t nstripes);

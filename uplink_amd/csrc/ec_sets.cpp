@@ -70,22 +70,28 @@ int set_segment(const ec_ctx *c, int nshares, const int *nums, const uint8_t *co
 constexpr unsigned kSetsHostFlags = hipHostMallocCoherent | hipHostMallocMapped;
 
 // A free slot of the ring with room for nseg segments and tgt_words words of
-// leaf tables (waits while kMaxSlots calls are in flight on the GPU).
+// leaf tables.  Waits while kMaxSlots live calls are in flight on the GPU, at
+// most kAcquireTimeoutMs; dead slots (a failed launch the device did not
+// recover from) do not count against the ring.  nullptr: no slot (timeout, or
+// no memory).
 SetsSlot *sets_acquire(ec_ctx *c, size_t nseg, size_t tgt_words) {
     SetsRing &R = c->sets;
     SetsSlot *sl = nullptr;
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(SetsRing::kAcquireTimeoutMs);
     for (;;) {
         {
             std::lock_guard<std::mutex> g(R.mu);
-            for (auto &x : R.slots)
-                if (x->idle()) {
-                    sl = x.get();
-                    break;
-                }
-            if (!sl && R.slots.size() < SetsRing::kMaxSlots) {
+            size_t live = 0;
+            for (auto &x : R.slots) {
+                live += !x->dead;
+                if (!sl && x->idle()) sl = x.get();
+            }
+            if (!sl && live < SetsRing::kMaxSlots) {
                 auto x = std::make_unique<SetsSlot>();
-                if (hipHostMalloc((void **)&x->h_words, 4 * 65, kSetsHostFlags) != hipSuccess) return nullptr;
-                memset(x->h_words, 0, 4 * 65);
+                if (hipHostMalloc((void **)&x->h_words, 4 * (SetsRing::kInitSegs + 1), kSetsHostFlags) != hipSuccess)
+                    return nullptr;
+                memset(x->h_words, 0, 4 * (SetsRing::kInitSegs + 1));
+                x->words_cap = SetsRing::kInitSegs + 1;
                 x->stage_cap = 0;
                 R.slots.push_back(std::move(x));
                 sl = R.slots.back().get();
@@ -93,36 +99,40 @@ SetsSlot *sets_acquire(ec_ctx *c, size_t nseg, size_t tgt_words) {
             if (sl) sl->busy = true;
         }
         if (sl) break;
+        if (std::chrono::steady_clock::now() > t_end) return nullptr;
         std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
-    // (the slot is ours, and the GPU is done with it: its buffers may be replaced)
+    // (the slot is ours, and the GPU is done with it: its buffers may be replaced; the ones it
+    // outgrows are kept until the slot goes, so no free synchronises the device here)
     bool ok = true;
     if (sl->stage_cap < nseg) {
-        const size_t cap = std::max<size_t>(32, (nseg + 31) & ~(size_t)31);
-        if (sl->h_stage) (void)hipHostFree(sl->h_stage);
-        if (sl->d_stage) (void)hipFree(sl->d_stage);
-        if (sl->d_desc) (void)hipFree(sl->d_desc);
-        if (sl->d_words) (void)hipFree(sl->d_words);
+        size_t cap = std::max(sl->stage_cap ? 2 * sl->stage_cap : SetsRing::kInitSegs, (size_t)32);
+        while (cap < nseg) cap *= 2;
+        if (sl->h_stage) sl->old_host.push_back(sl->h_stage);
+        for (void *p : {(void *)sl->d_stage, (void *)sl->d_desc, (void *)sl->d_words})
+            if (p) sl->old_dev.push_back(p);
         sl->h_stage = nullptr, sl->d_stage = nullptr, sl->d_desc = nullptr, sl->d_words = nullptr;
         ok = hipHostMalloc((void **)&sl->h_stage, cap * sizeof(SetStage),
                            c->sets_stage_dma ? hipHostMallocDefault : kSetsHostFlags) == hipSuccess &&
              (!c->sets_stage_dma || hipMalloc(&sl->d_stage, cap * sizeof(SetStage)) == hipSuccess) &&
              hipMalloc(&sl->d_desc, cap * sizeof(SetDesc)) == hipSuccess &&
              hipMalloc(&sl->d_words, 4 * (cap + 1)) == hipSuccess;
-        if (ok && cap + 1 > 65) {
+        if (ok && cap + 1 > sl->words_cap) {
             uint32_t *hw = nullptr;
             ok = hipHostMalloc((void **)&hw, 4 * (cap + 1), kSetsHostFlags) == hipSuccess;
             if (ok) {
                 hw[0] = sl->seq;
-                (void)hipHostFree(sl->h_words);
+                sl->old_host.push_back(sl->h_words);
                 sl->h_words = hw;
+                sl->words_cap = cap + 1;
             }
         }
         sl->stage_cap = ok ? cap : 0;
     }
     if (ok && sl->tgt_cap < tgt_words) {
-        const size_t cap = std::max<size_t>(tgt_words, (size_t)32 * 8192);
-        if (sl->d_tgt) (void)hipFree(sl->d_tgt);
+        size_t cap = std::max(sl->tgt_cap ? 2 * sl->tgt_cap : SetsRing::kInitTgtWords, (size_t)1);
+        while (cap < tgt_words) cap *= 2;
+        if (sl->d_tgt) sl->old_dev.push_back(sl->d_tgt);
         sl->d_tgt = nullptr;
         ok = hipMalloc(&sl->d_tgt, cap * 8) == hipSuccess;
         sl->tgt_cap = ok ? cap : 0;
@@ -176,6 +186,9 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
         toff[q] = words;
         words += (sets_tgt_entries(segs[idx[q]].nin, segs[idx[q]].rows, segs[idx[q]].nw) + 7) & ~(size_t)7;
     }
+    // the completion-word protocol needs the launches to run: not under stream capture
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return EC_ERR_UNSUPPORTED;
     SetsSlot *sl = sets_acquire(c, nseg, words);
     if (!sl) return EC_ERR_DEVICE;
     // one segment: its record goes in the prep launch's arguments (no read over the bus)
@@ -238,9 +251,14 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
         e = launch_matmul_sets(a, segs[idx[q0]].nw, s);
         q0 = q1;
     }
-    if (e != hipSuccess) {  // the slot may be half used: never again
+    if (e != hipSuccess) {
+        // the slot's prep (and maybe a class launch) is queued but its completion
+        // word will never be written: once the stream has run what was queued, the
+        // slot is free again (the next call's prep zeroes its counter); if the
+        // device does not get there, the slot is never reused
+        const bool drained = hipStreamSynchronize(s) == hipSuccess;
         std::lock_guard<std::mutex> g(c->sets.mu);
-        sl->dead = true;
+        sl->dead = !drained;
         sl->busy = false;
         return hip_fail(e);
     }

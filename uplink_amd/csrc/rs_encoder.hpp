@@ -103,6 +103,9 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
         const uint32_t x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
         if constexpr ((DIAG & 16) != 0) {  // kDiagNoRowOps
             asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+            // the rows stored are the chunk's last input (random bytes, as real parity is)
+            if constexpr (JJ + 1 == JN)
+                static_for<OPW>([&]<int O>() { static_for<8>([&]<int P>() { acc[O][P] = x[P]; }); });
             return;
         }
         uint32_t lo[16], hi[16];
@@ -169,7 +172,9 @@ __device__ __forceinline__ int32_t take_tile(const RsArgs &a, int m) {
 //   kDiagNoCombos         timing only: the 22 combination planes per input are
 //                         not built (every combination reads a single plane)
 //   kDiagNoRowOps         timing only: no multiply-add at all (the inputs' planes
-//                         are read from the LDS and kept live, the rows stay zero)
+//                         are read from the LDS and kept live; each row stored is
+//                         the tile's last input); the library builds this form
+//                         for RS(29,80) as its on-box ceiling (rs_encode_probe.hip)
 //   kDiagHalfCombos       timing only: kDiagNoCombos for the odd inputs (what
 //                         building each input's combinations in half the waves saves)
 //   kDiagLdsCombos        timing only: the 30 combination planes of each input read

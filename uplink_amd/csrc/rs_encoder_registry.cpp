@@ -273,10 +273,10 @@ std::string device_arch(int dev) {
 
 }  // namespace
 
-// Start (if needed) the run-time compilation of (k, n); with `wait`, block
-// until it is done.  Returns the encoder when it is loaded on the current
-// device, else nullptr.
-const EncoderKernel *jit_encoder(int k, int n, bool wait) {
+// Start (if needed and `start`) the run-time compilation of (k, n); with
+// `wait`, block until it is done.  Returns the encoder when it is loaded on
+// the current device, else nullptr.
+const EncoderKernel *jit_encoder(int k, int n, bool wait, bool start) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     const std::string arch = device_arch(dev);
@@ -285,6 +285,7 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
     auto key = std::make_tuple(arch, k, n);
     auto it = g_jit.find(key);
     if (it == g_jit.end()) {
+        if (!start) return nullptr;
         JitEntry *e = new JitEntry();
         g_jit.emplace(key, std::unique_ptr<JitEntry>(e));
         static std::once_flag once;
@@ -316,7 +317,7 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
             g_cv.wait(g, [&] { return e->state != JitEntry::kCompiling; });
             if (e->state == JitEntry::kReady) {
                 g.unlock();
-                return jit_encoder(k, n, false);
+                return jit_encoder(k, n, false, false);
             }
         }
         fprintf(stderr, "uplink_ec: loading the RS(%d,%d) encoder failed\n", k, n);
@@ -345,10 +346,11 @@ const EncoderKernel *jit_encoder(int k, int n, bool wait) {
 constexpr int kJitMaxK = 48;
 
 // UPLINK_EC_JIT=0: no run-time compilation at all (library-built encoders and
-// the runtime-matrix kernel only).  A process that starts a compile waits for
-// it at exit (join_compiles), and a cold compile takes minutes on a box's CPU
-// share: the plain-C ABI client sets this (tests/test_c_abi.py), since its
-// RS(10,20) per-stripe encodes would otherwise start one.
+// the runtime-matrix kernel only).  Otherwise a compile starts only for a
+// caller that asks for it (find_encoder's `start`: whole-segment launches of
+// at least kJitMinTiles tiles, and ec_prepare_encoder), never for per-stripe
+// work, which the runtime-matrix kernel serves at the same speed; a process
+// that started one waits at exit for the one in progress (join_compiles).
 bool jit_allowed() {
     static const bool on = [] {
         const char *e = getenv("UPLINK_EC_JIT");
@@ -357,10 +359,10 @@ bool jit_allowed() {
     return on;
 }
 
-const EncoderKernel *find_encoder(int k, int n, bool wait) {
+const EncoderKernel *find_encoder(int k, int n, bool wait, bool start) {
     if (const EncoderKernel *e = aot_encoder(k, n)) return e;
     if (!enc::supported(k, n) || k > kJitMaxK || !jit_allowed()) return nullptr;
-    return jit_encoder(k, n, wait);
+    return jit_encoder(k, n, wait, start || wait);
 }
 
 hipError_t launch_encode_special(const EncoderKernel &e, const RsArgs &args, int grid, hipStream_t s) {

@@ -29,11 +29,17 @@ struct EncoderKernel {
 };
 
 // The encoder for (k, n) on the current device, or nullptr when (k, n) is
-// outside the compile-time encoder's limits or run-time compilation failed
-// (the caller then uses the runtime-matrix kernel).  Thread-safe.
-const EncoderKernel *find_encoder(int k, int n, bool wait = false);
+// outside the compile-time encoder's limits, its run-time compilation is not
+// done (or failed), or -- `start` false -- has not been started (the caller
+// then uses the runtime-matrix kernel).  A compilation is started only for a
+// caller that passes `start` (launches large enough to pay for it, and
+// ec_prepare_encoder); `wait` blocks until it is done.  Thread-safe.
+const EncoderKernel *find_encoder(int k, int n, bool wait = false, bool start = true);
 // Library-built encoders (rs_encoder_registry.cpp); nullptr if none.
 const EncoderKernel *aot_encoder(int k, int n);
+// RS(29,80)'s encoder without its arithmetic (rs_encode_probe.hip): the
+// on-box ceiling of the encoder's own access pattern; nullptr for other codes.
+const EncoderKernel *shape_probe_encoder(int k, int n);
 // The same limits find_encoder applies (no compilation).
 bool encoder_supported(int k, int n);
 hipError_t launch_encode_special(const EncoderKernel &e, const RsArgs &args, int grid, hipStream_t stream);

@@ -239,6 +239,10 @@ class SegmentPieceReader:
 
     def _prepare(self):
         with self._mu:
+            # after close() nothing may be allocated or begun again (the buffers went back to
+            # the pool; a new upload would only be reclaimed by __del__)
+            if self._closing:
+                raise EEStreamError("piece reader used after close")
             if self._padded is not None:
                 return
             rs = self.redundancy
