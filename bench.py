@@ -14,9 +14,9 @@ One step = every rank processes its whole shard once, in launches of
      of its pieces in a share set of its own -- the way uplink downloads: every
      segment from whichever 29 pieces answered first (stripe.go:314-354), one
      GetWithOptions per segment (client.go:273-308).  Every timed launch gets
-     32 fresh seeded 29-subsets (its first segment the all-parity {51..79},
-     the worst case); no decode plan is made or warmed (the decode rows are
-     solved on the GPU inside the call, rs_sets.hip).
+     32 fresh seeded 29-subsets (every step's first segment from the
+     all-parity {51..79}, the worst case); no decode plan is made or warmed
+     (the decode rows are solved on the GPU inside the call, rs_sets.hip).
 The segments are synthetic (device-generated random bytes, PadReader-padded to
 9040 stripes x 29 x 256 B), from a pool of 2 x 32 distinct segments per rank
 cycled over the shard: 1024 segments' pieces would not fit one GPU (SURVEY §8d
@@ -105,11 +105,15 @@ def share_sets():
     return sets
 
 
-def fresh_launch_sets(seed: int, nb: int):
+def fresh_launch_sets(seed: int, nb: int, all_parity_first: bool):
     """The share sets of one timed decode launch: nb fresh seeded 29-subsets,
-    the first of them the all-parity {51..79} (worst case)."""
+    with all_parity_first the first of them the all-parity {51..79} (the
+    worst case: 29 rows to compute)."""
     rng = np.random.default_rng(seed)
-    return [list(range(N - K, N))] + [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(nb - 1)]
+    sets = [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(nb)]
+    if all_parity_first:
+        sets[0] = list(range(N - K, N))
+    return sets
 
 
 def cgroup_cpus():
@@ -650,13 +654,13 @@ def main():
     seed_base = 0x5E750000 + 1_000_003 * rank
     launch_no = [0]
 
-    def fresh_args(slot, nb):
-        a = set_args(slot, fresh_launch_sets(seed_base + launch_no[0], nb))
+    def fresh_args(slot, nb, all_parity_first=False):
+        a = set_args(slot, fresh_launch_sets(seed_base + launch_no[0], nb, all_parity_first))
         launch_no[0] += 1
         return a
 
-    def step_args():
-        return [fresh_args(b % pool, nb) for b, nb in enumerate(launches)]
+    def step_args():  # (every step's first segment is rebuilt from {51..79})
+        return [fresh_args(b % pool, nb, b == 0) for b, nb in enumerate(launches)]
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -738,7 +742,7 @@ def main():
     for slot in range(pool):
         outs[slot].zero_()
         encode(slot, B)
-        decode(slot, fresh_args(slot, B))
+        decode(slot, fresh_args(slot, B, True))
         torch.cuda.synchronize(dev)
         verified = verified and bool(torch.equal(outs[slot], segs[slot]))
     verified = verified and oracle_spot_check(pieces[0][0], segs[0][0])
@@ -893,8 +897,8 @@ def main():
                                "(BASELINE configs[3], each segment as configs[1]+[2])",
                    "k": K, "n": N, "erasure_share_size": ESS, "total_segments_per_step": args.total_segments,
                    "segments_this_rank": count, "segments_per_launch": B, "stripes_per_segment": NSTRIPES,
-                   "decode_share_sets": "a fresh seeded 29-subset per segment and launch (each launch's first "
-                                        "segment {51..79}); no plan made or warmed",
+                   "decode_share_sets": "a fresh seeded 29-subset per segment and launch (each step's first "
+                                        "segment from {51..79}); no plan made or warmed",
                    "parallelism": f"segments sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(dk["achieved_GBps"], 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(dk["achieved_GBps"] / HBM_PEAK_GBPS, 4),

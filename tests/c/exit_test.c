@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "uplink_ec.h"
 
@@ -41,6 +42,10 @@ int main(int argc, char **argv) {
         fprintf(stderr, "RS(%d,%d)'s encoder was already compiled: the test needs an empty cache\n", k, n);
         return 5;
     }
+    /* let the compile thread get going (a compile still queued when exit starts is skipped,
+     * not waited for); it takes ~1 s or more cold, so it is still running when main returns */
+    struct timespec ts = {0, 100 * 1000 * 1000};
+    nanosleep(&ts, NULL);
     printf("returning from main while RS(%d,%d)'s encoder compiles\n", k, n);
     return 0;
 }

@@ -53,9 +53,12 @@ res = {
               "over dispatches; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; tools/pmc_traffic.py",
     "segments_per_launch": B,
     "encode": family("rs_encode_special<29, 80, 8, 4, true>"),
-    "decode": family("rs_matmul_dma"),  # the straight-line rebuild (a plan's first launch: rs_matmul_jt)
+    # the timed decode: the share-set pass (one rs_matmul_sets launch per call of 32 segments, each with
+    # a set of its own; its rs_sets_prep moves a few KB); the warm shared-set leg's straight-line rebuild
+    "decode": family("rs_matmul_sets"),
+    "decode_warm_shared_set": family("rs_matmul_dma"),
     "encode_parity_only": family("rs_encode_special<29, 80, 8, 4, false>"),
-    "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD,
+    "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD, "decode_warm_shared_set": 2 * B * S_PAD,
                     "encode_parity_only": int(B * S_PAD * (1 + (N - K) / K))},
 }
 json.dump(res, open(out, "w"), indent=1)

@@ -54,6 +54,25 @@ using namespace dev;
 #ifndef UPLINK_ENC_WGS
 #define UPLINK_ENC_WGS 1
 #endif
+// The loaders issue an item's copy-through stores one item late: after the
+// next item's LDS-DMAs instead of while slicing (the raw bytes kept in
+// registers meanwhile), so the counted vmcnt wait for those DMAs does not
+// also wait for the item's own stores.  0 = store while slicing (A/B builds).
+#ifndef UPLINK_ENC_DEFER_COPY
+#define UPLINK_ENC_DEFER_COPY 1
+#endif
+// Each compute wave stores up to this many of a tile's parity rows one 16-byte
+// store at a time between the next tile's first inputs instead of in the
+// burst at the tile's end (the rows kept in registers meanwhile).
+#ifndef UPLINK_ENC_DEFER_ROWS
+#define UPLINK_ENC_DEFER_ROWS 0
+#endif
+// The compute waves meet the item's barrier right after their last read of
+// the slot and store the tile's parity rows after it (while the loaders issue
+// the next item's LDS-DMAs), instead of storing first and then meeting it.
+#ifndef UPLINK_ENC_LATE_STORES
+#define UPLINK_ENC_LATE_STORES 0
+#endif
 constexpr int kSlots = UPLINK_ENC_SLOTS;
 constexpr int kAhead = kSlots - 1;               // items between a load's issue and that item's multiply
 constexpr int kMaxChunk = UPLINK_ENC_MAX_CHUNK;  // input shares per item
@@ -68,8 +87,8 @@ constexpr int rbase_of(int R, int NC, int W) { return W * (R / NC) + (W < R % NC
 // acc[O] ^= G[K + rbase + O][J] * x_J for the wave's rows and the inputs
 // J0 .. J0+JN-1, whose bit planes sit at slot position J - J0 (planes 0-3 of a
 // lane as one 16-byte word at 16 lane, planes 4-7 at 1024 + 16 lane).
-template <int K, int N, int NC, int OPW, int W, int J0, int JN, int DIAG = 0>
-__device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint32_t (&acc)[OPW][8]) {
+template <int K, int N, int NC, int OPW, int W, int J0, int JN, int DIAG = 0, typename Hook>
+__device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint32_t (&acc)[OPW][8], Hook &&hook) {
     // The plane reads are the same in every wave's arm of the caller's switch;
     // an offset the compiler cannot see through keeps it from hoisting them out
     // of the arms (all of a chunk's planes live at once would spill).  One
@@ -106,6 +125,7 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
             // the rows stored are the chunk's last input (random bytes, as real parity is)
             if constexpr (JJ + 1 == JN)
                 static_for<OPW>([&]<int O>() { static_for<8>([&]<int P>() { acc[O][P] = x[P]; }); });
+            hook.template operator()<JJ>();
             return;
         }
         uint32_t lo[16], hi[16];
@@ -147,6 +167,7 @@ __device__ __forceinline__ void compute_chunk(const u32x4 *slot, int lane, uint3
                 });
             }
         });
+        hook.template operator()<JJ>();
     });
 }
 
@@ -197,7 +218,8 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
     constexpr int PER = (KC + NL - 1) / NL;
     constexpr int A = kAhead;
     // a loader waits with at most 2(A-1) items of its DMAs and copy-through stores issued after the awaited ones
-    static_assert(4 * (A - 1) * PER <= 63 && A >= 1, "a loader's VMEM ops in flight must fit the vmcnt counter");
+    static_assert(4 * (A - 1) * PER <= 63 && 2 * (2 * A - 1) * PER <= 63 && A >= 1,
+                  "a loader's VMEM ops in flight must fit the vmcnt counter");
     constexpr int SLOT = KC * 2048;  // bytes
     static_assert(kSlots * SLOT <= 150 * 1024, "LDS ring too large");
     // Tile m (items m*NCH ..) is taken by compute wave 0 at the start of item
@@ -253,14 +275,36 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
             }
         }
     };
+    // loader: the copy-through stores of item (t, ch), the raw bytes of this
+    // wave's inputs -- two stores per input on every lane, so the wave's count of
+    // VMEM ops is exact (a lane past the end of the batch holds column 0 of its
+    // share, which it stores to column 0 of that share's piece: the bytes already
+    // there)
+    auto copy_out = [&](int64_t t, int ch, const u32x4 *rA, const u32x4 *rB) {
+        const TileCols c = pair_cols(a, t, lane);
+        const int j0 = ch * KC, jn = K - j0 < KC ? K - j0 : KC;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int j = lw + NL * i;
+            if (j < jn) {
+                if constexpr ((DIAG & kDiagNoCopyStores) != 0) {
+                    sink16(rA[i].x, rA[i].y, rA[i].z, rA[i].w);
+                    sink16(rB[i].x, rB[i].y, rB[i].z, rB[i].w);
+                } else {
+                    uint8_t *p = a.out_base + a.copy_off[j0 + j];
+                    uint8_t *qa = p + (c.vA ? c.outA : 0), *qb = p + (c.vB ? c.outB : 0);
+                    if (in_range(a, qa, true, 2)) st16<true>(qa, rA[i].x, rA[i].y, rA[i].z, rA[i].w);
+                    if (in_range(a, qb, true, 2)) st16<true>(qb, rB[i].x, rB[i].y, rB[i].z, rB[i].w);
+                }
+            }
+        }
+    };
+    constexpr bool kDefer = do_copy && UPLINK_ENC_DEFER_COPY != 0;
     // loader: item (t, ch) in slot sl from raw bytes to bit planes, in place (each
     // lane rewrites its own 32 bytes); the systematic shares go to their data
-    // pieces on the way -- two stores per input on every lane, so the wave's
-    // count of VMEM ops is exact (a lane past the end of the batch holds column
-    // 0 of its share, which it stores to column 0 of that share's piece: the
-    // bytes already there)
-    auto slice = [&](int sl, int64_t t, int ch) {
-        const TileCols c = pair_cols(a, t, lane);
+    // pieces on the way -- or, kDefer, the raw bytes are kept in rA / rB for
+    // their stores one item later (the loop below)
+    auto slice = [&](int sl, int64_t t, int ch, u32x4 *rA, u32x4 *rB) {
         const int j0 = ch * KC, jn = K - j0 < KC ? K - j0 : KC;
         u32x4 *slot = ring + sl * (SLOT / 16);
 #pragma unroll
@@ -268,14 +312,20 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
             const int j = lw + NL * i;
             if (j < jn) {
                 const u32x4 A4 = slot[j * 128 + lane], B4 = slot[j * 128 + 64 + lane];
-                if constexpr (do_copy && (DIAG & kDiagNoCopyStores) != 0) {
-                    sink16(A4.x, A4.y, A4.z, A4.w);
-                    sink16(B4.x, B4.y, B4.z, B4.w);
+                if constexpr (kDefer) {
+                    rA[i] = A4;
+                    rB[i] = B4;
                 } else if constexpr (do_copy) {
-                    uint8_t *p = a.out_base + a.copy_off[j0 + j];
-                    uint8_t *qa = p + (c.vA ? c.outA : 0), *qb = p + (c.vB ? c.outB : 0);
-                    if (in_range(a, qa, true, 2)) st16<true>(qa, A4.x, A4.y, A4.z, A4.w);
-                    if (in_range(a, qb, true, 2)) st16<true>(qb, B4.x, B4.y, B4.z, B4.w);
+                    const TileCols c = pair_cols(a, t, lane);
+                    if constexpr ((DIAG & kDiagNoCopyStores) != 0) {
+                        sink16(A4.x, A4.y, A4.z, A4.w);
+                        sink16(B4.x, B4.y, B4.z, B4.w);
+                    } else {
+                        uint8_t *p = a.out_base + a.copy_off[j0 + j];
+                        uint8_t *qa = p + (c.vA ? c.outA : 0), *qb = p + (c.vB ? c.outB : 0);
+                        if (in_range(a, qa, true, 2)) st16<true>(qa, A4.x, A4.y, A4.z, A4.w);
+                        if (in_range(a, qb, true, 2)) st16<true>(qb, B4.x, B4.y, B4.z, B4.w);
+                    }
                 }
                 uint32_t w[8] = {A4.x, A4.y, A4.z, A4.w, B4.x, B4.y, B4.z, B4.w};
                 bitslice8(w);
@@ -313,6 +363,7 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
             }
         }
     };
+    static_assert(!kDefer || A == 1, "deferred copy-through stores are counted for a ring of 2 slots");
     if (loader) {
         // items 0 .. A-1 in flight, item 0 bit-sliced
         int after = 0;
@@ -327,33 +378,50 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
         const int64_t t0 = tile_of(0);
         if (t0 < P) {
             wait_vm(after);
-            slice(0, t0, 0);
+            // (item 0's copy-through stores at once: nothing of the loader's is
+            // live across the barrier below)
+            u32x4 rA0[kDefer ? PER : 1], rB0[kDefer ? PER : 1];
+            slice(0, t0, 0, rA0, rB0);
+            if constexpr (kDefer) copy_out(t0, 0, rA0, rB0);
         }
     }
     barrier_w();
     if (loader) {
+        // (kDefer) the raw bytes of the item sliced last (from item 1 on), its tile and chunk
+        [[maybe_unused]] u32x4 rawA[kDefer ? PER : 1], rawB[kDefer ? PER : 1];
+        [[maybe_unused]] int64_t raw_t = 0;
+        [[maybe_unused]] int raw_ch = 0;
         for (int i = 0;; i++) {
             if (tile_of(i) >= P) break;
             const int64_t ua = tile_of(i + A);
             if (ua < P) issue((i + A) % kSlots, ua, (i + A) % NCH);
+            // (kDefer) item i's copy-through stores, behind item i+1's DMAs
+            if constexpr (kDefer)
+                if (i > 0) copy_out(raw_t, raw_ch, rawA, rawB);
             const int64_t u1 = tile_of(i + 1);
             if (u1 < P) {
                 // this wave's VMEM ops issued after item i+1's DMAs: the copy-through
-                // stores of items i+2-A .. i (sliced since) and the DMAs of items
-                // i+2 .. i+A; completion is in order, so waiting down to that many
-                // means item i+1 has landed
+                // stores of items i+2-A .. i (sliced since; kDefer: item i's, issued
+                // just now, from item 1 on) and the DMAs of items i+2 .. i+A;
+                // completion is in order, so waiting down to that many means item i+1
+                // has landed
                 int after = 0;
-                if constexpr (do_copy && kCountStores)
+                if constexpr (do_copy && kCountStores && kDefer) {
+                    if (i > 0) after += ops_of(i % NCH);
+                } else if constexpr (do_copy && kCountStores) {
 #pragma unroll
                     for (int y = i + 2 - A; y <= i; y++)
                         if (y >= 0) after += ops_of(y % NCH);
+                }
 #pragma unroll
                 for (int y = i + 2; y <= i + A; y++)
                     if (tile_of(y) < P) after += ops_of(y % NCH);
                 const uint64_t tw = d_now();
                 wait_vm(after);
                 if constexpr ((DIAG & kDiagStamp) != 0) d_wait += d_now() - tw;
-                slice((i + 1) % kSlots, u1, (i + 1) % NCH);
+                slice((i + 1) % kSlots, u1, (i + 1) % NCH, rawA, rawB);
+                raw_t = u1;
+                raw_ch = (i + 1) % NCH;
             }
             barrier_w();
         }
@@ -363,6 +431,23 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
     // compute waves: per tile, the chunks in order with a barrier after each (the
     // loaders' per-item barrier); the accumulators live across the chunks
     uint32_t acc[OPW][8];
+    // deferred parity rows (UPLINK_ENC_DEFER_ROWS): the first DR rows of the
+    // previous tile, un-bit-sliced, stored between the next tile's first 2 DR inputs
+    constexpr int DR = (DIAG & kDiagNoParityStores) != 0 ? 0
+                       : UPLINK_ENC_DEFER_ROWS < OPW ? UPLINK_ENC_DEFER_ROWS : OPW;
+    [[maybe_unused]] uint32_t dfr[DR > 0 ? DR : 1][8];
+    [[maybe_unused]] TileCols dc{};
+    [[maybe_unused]] int dcnt = 0;  // deferred rows held (0: none)
+    const int w_rbase = rbase_of(R, NC, wave), w_rows = rows_of(R, NC, wave);
+    constexpr bool kLateStores = UPLINK_ENC_LATE_STORES != 0;
+    auto store_half = [&](const uint32_t (&w)[8], int row, const TileCols &c, bool second) __attribute__((always_inline)) {
+        uint8_t *p = a.out_base + a.out_off[row];
+        if (!second) {
+            if (c.vA && in_range(a, p + c.outA, true, 3)) st16<true>(p + c.outA, w[0], w[1], w[2], w[3]);
+        } else {
+            if (c.vB && in_range(a, p + c.outB, true, 3)) st16<true>(p + c.outB, w[4], w[5], w[6], w[7]);
+        }
+    };
     for (int m = 0;; m++) {
         const int64_t ti = tile_of(m * NCH);
         if (ti >= P) break;
@@ -370,7 +455,7 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
         for (int o = 0; o < OPW; o++)
 #pragma unroll
             for (int p = 0; p < 8; p++) acc[o][p] = 0;
-        static_for<NCH>([&]<int C>() {
+        static_for<NCH>([&]<int C>() __attribute__((always_inline)) {
             const int i = m * NCH + C;
             // the tile of item i+A+1 onwards (when one starts there): its queue atomic
             // returns during this item's multiply and is published before the barrier
@@ -382,20 +467,54 @@ __device__ __forceinline__ void encode_body(const RsArgs &a) {
             }
             constexpr int J0 = C * KC, JN = K - J0 < KC ? K - J0 : KC;
             const u32x4 *slot = ring + (i % kSlots) * (SLOT / 16);
-            static_for<NC>([&]<int W>() {
-                if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN, DIAG>(slot, lane, acc);
+            // (DR) the previous tile's deferred rows, half a row after each of the first 2 DR inputs
+            auto hook = [&]<int JJ>() __attribute__((always_inline)) {
+                if constexpr (DR > 0 && C == 0 && JJ < 2 * DR)
+                    if (JJ / 2 < dcnt) store_half(dfr[JJ / 2], w_rbase + JJ / 2, dc, (JJ & 1) != 0);
+            };
+            static_for<NC>([&]<int W>() __attribute__((always_inline)) {
+                if (wave == W) compute_chunk<K, N, NC, OPW, W, J0, JN, DIAG>(slot, lane, acc, hook);
             });
             if (pend_m >= 0) s_q[pend_m & 7] = pending;
+            // (kLateStores) the barrier first: the slot is read to the end, so the
+            // loaders' next LDS-DMAs go out before this tile's burst of parity stores
+            if constexpr (kLateStores) barrier_w();
             if constexpr (C == NCH - 1) {
                 const TileCols c = pair_cols(a, ti, lane);
-                if constexpr ((DIAG & kDiagNoParityStores) != 0)
-                    sink_rows<OPW>(rows_of(R, NC, wave), acc);
-                else
-                    store_rows<OPW, true>(a, 0, c, rbase_of(R, NC, wave), rows_of(R, NC, wave), acc);
+                if constexpr ((DIAG & kDiagNoParityStores) != 0) {
+                    sink_rows<OPW>(w_rows, acc);
+                } else if constexpr (DR > 0) {
+                    static_for<OPW>([&]<int O>() {
+                        if (O < w_rows) {
+                            uint32_t w[8];
+#pragma unroll
+                            for (int p = 0; p < 8; p++) w[p] = acc[O][p];
+                            unbitslice8(w);
+                            if constexpr (O < DR) {
+#pragma unroll
+                                for (int p = 0; p < 8; p++) dfr[O][p] = w[p];
+                            } else {
+                                store_half(w, w_rbase + O, c, false);
+                                store_half(w, w_rbase + O, c, true);
+                            }
+                        }
+                    });
+                    dc = c;
+                    dcnt = w_rows < DR ? w_rows : DR;
+                } else {
+                    store_rows<OPW, true>(a, 0, c, w_rbase, w_rows, acc);
+                }
             }
-            barrier_w();
+            if constexpr (!kLateStores) barrier_w();
         });
     }
+    if constexpr (DR > 0)  // the last tile's deferred rows
+        static_for<DR>([&]<int O>() {
+            if (O < dcnt) {
+                store_half(dfr[O], w_rbase + O, dc, false);
+                store_half(dfr[O], w_rbase + O, dc, true);
+            }
+        });
     if (wave == 0) stamp_out(0);
     // The launch's last workgroup to finish zeroes the queue for the next launch
     // that gets it (so none needs a memset before it).  Every take of this
