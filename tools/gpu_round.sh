@@ -23,7 +23,7 @@ mkdir -p $O
 for step in "$@"; do
   echo "[$(date +%T)] $step" >> $O/steps.log
   case $step in
-    tests) timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu > $O/pytest_gpu.log 2>&1 ;;
+    tests) timeout -k 10 900 python -u -m pytest -x -q --durations=25 --timeout 200 --timeout-method thread tests -m gpu > $O/pytest_gpu.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 ;;
     bench) timeout -k 10 500 python -u bench.py > $O/bench.log 2>&1 ;;
     prof) bash tools/prof_round.sh $OUT ;;
