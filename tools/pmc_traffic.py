@@ -15,17 +15,19 @@ K, N, S_PAD = 29, 80, 9040 * 29 * 256
 
 
 def per_kernel(d, counter):
+    """counter value per dispatch, by kernel name, with the dispatch's grid (workgroups)"""
     vals = defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         acc = defaultdict(float)
-        names = {}
+        names, grid = {}, {}
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
             acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"]
+            grid[r["Dispatch_Id"]] = int(r["Grid_Size"]) // max(int(r["Workgroup_Size"]), 1)  # workgroups
         for dsp, v in acc.items():
-            vals[names[dsp]].append(v)
+            vals[names[dsp]].append((grid[dsp], v))
     return vals
 
 
@@ -33,9 +35,16 @@ fetch = per_kernel(fetch_dir, "FETCH_SIZE")
 write = per_kernel(write_dir, "WRITE_SIZE")
 
 
-def family(match):
-    f = [v for k, vs in fetch.items() if match in k for v in vs]
-    w = [v for k, vs in write.items() if match in k for v in vs]
+def family(match, full_grid=False):
+    """mean per dispatch over the kernels whose name contains match; full_grid: only the
+    dispatches of the largest grid seen (the share-set kernel launches one workgroup per tile,
+    so a grid that size is a whole B-segment call; the bench's other legs make smaller ones)"""
+    f = [gv for k, vs in fetch.items() if match in k for gv in vs]
+    w = [gv for k, vs in write.items() if match in k for gv in vs]
+    if full_grid:
+        g = max(x for x, _ in f)
+        f, w = [gv for gv in f if gv[0] == g], [gv for gv in w if gv[0] == g]
+    f, w = [v for _, v in f], [v for _, v in w]
     names = sorted({k for k in fetch if match in k})
     fk, wk = sum(f) / len(f), sum(w) / len(w)
     rd, wr = 2 * fk * 1024, wk * 1024
@@ -55,7 +64,7 @@ res = {
     "encode": family("rs_encode_special<29, 80, 8, 4, true>"),
     # the timed decode: the share-set pass (one rs_matmul_sets launch per call of 32 segments, each with
     # a set of its own; its rs_sets_prep moves a few KB); the warm shared-set leg's straight-line rebuild
-    "decode": family("rs_matmul_sets"),
+    "decode": family("rs_matmul_sets", full_grid=True),
     "decode_warm_shared_set": family("rs_matmul_dma"),
     "encode_parity_only": family("rs_encode_special<29, 80, 8, 4, false>"),
     "algorithmic": {"encode": int(B * S_PAD * (1 + N / K)), "decode": 2 * B * S_PAD, "decode_warm_shared_set": 2 * B * S_PAD,
