@@ -445,8 +445,9 @@ def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 16):
     jump-table body).  Outside the timed region, informational:
       * "32 segments, 32 fresh seeded 29-subsets per launch": HIP-event time per
         call, calls back to back, and its HBM fraction (2 x S_pad per segment);
-      * "one segment, fresh set": wall clock per call, launch to synchronised
-        (median), and the stream time of such calls back to back."""
+      * "one segment, fresh set": wall clock per call, from the call to its
+        stream synchronised (median), and the stream time of such calls back
+        to back."""
     rng = np.random.default_rng(3229)
     segs = torch.randint(0, 256, (nb, S_PAD), dtype=torch.uint8, device=dev)
     pcs = torch.empty((nb, N, PIECE), dtype=torch.uint8, device=dev)
@@ -507,7 +508,7 @@ def fresh_sets_leg(L, ctx, dev, sptr, nb: int = 32, reps: int = 16):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         go(one)
-        torch.cuda.synchronize(dev)
+        stream.synchronize()  # (the caller's stream, as a Go caller waits for its own call: hipStreamSynchronize)
         walls.append(time.perf_counter() - t0)
     singles = [prep(fresh(1)) for _ in range(reps)]
     torch.cuda.synchronize(dev)

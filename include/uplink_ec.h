@@ -339,10 +339,14 @@ int ec_set_device(int device);
  * (n == k) */
 const char *ec_encode_kernel_name(const ec_ctx *ctx);
 /* The compile-time-G encoder of a (k, n) that is not built into the library
- * is compiled in the background from its first encode call (or this call) on
- * (hiprtc; the code object is cached on disk); until it is ready the encode
- * calls use the runtime-matrix kernel, with identical results.  Returns 1 when it is ready (with wait != 0:
- * after waiting for the compilation), 0 when this (k, n) has none. */
+ * is compiled in the background from its first whole-segment encode call (at
+ * least 256 tiles: a few MiB of stripes) or this call on (hiprtc, ~1 s; the
+ * code object is cached on disk); per-stripe and few-stripe calls never start
+ * one.  Until it is ready the encode calls use the runtime-matrix kernel, with
+ * identical results.  A process that started a compile waits at exit for the
+ * one in progress.  Returns 1 when it is ready (with wait != 0: after waiting
+ * for the compilation), 0 when this (k, n) has none.  UPLINK_EC_JIT=0 in the
+ * environment turns run-time compilation off. */
 int ec_prepare_encoder(const ec_ctx *ctx, int wait);
 /* Body of the runtime-matrix kernel for this ctx's decode (and other
  * runtime-matrix) plans, DESIGN.md §4 "Straight-line rebuild":

@@ -12,6 +12,7 @@
 #   sets       tools/bench_sets.py (share-set calls)
 #   segment    tools/bench_segment.py (streamed upload)
 #   lib=PATH   A/B: bench.py against another build of the library (--lib PATH)
+#   batch=B    bench.py with B segments per launch (--batch B)
 #   trace      a short bench.py under rocprofv3 --kernel-trace --stats (per-dispatch times)
 #   py=SCRIPT  any other python script under tools/ (args after a colon: py=tools/x.py:--a:1)
 set -e
@@ -30,6 +31,7 @@ for step in "$@"; do
     sets) timeout -k 10 200 python -u tools/bench_sets.py > $O/bench_sets.json 2> $O/bench_sets.err ;;
     segment) timeout -k 10 200 python -u tools/bench_segment.py > $O/bench_segment.log 2>&1 ;;
     lib=*) timeout -k 10 500 python -u bench.py --lib ${step#lib=} --no-cpu-baseline --no-other-configs >> $O/bench_lib.log 2>&1 ;;
+    batch=*) timeout -k 10 500 python -u bench.py --batch ${step#batch=} --no-cpu-baseline --no-other-configs >> $O/bench_batch.log 2>&1 ;;
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-other-configs > $O/bench_trace.log 2>&1 ;;
     py=*) spec=${step#py=}; IFS=: read -ra a <<< "$spec"
           timeout -k 10 600 python -u "${a[@]}" >> $O/$(basename ${a[0]} .py).log 2>&1 ;;
