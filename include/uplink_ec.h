@@ -170,6 +170,8 @@ int ec_decode_segments_batched(const ec_ctx *ctx, int nshares, const int *nums, 
  * choice is infectious Rebuild's per segment.  The decode rows of every
  * segment are solved on the GPU in stream order; the host only chooses the
  * shares (no synchronisation, no plan, no code generation on the call path).
+ * A Rebuild of one segment (up to 64 shares) is one launch whose decode rows
+ * the host solves and passes in the launch's arguments.
  *
  * ec_rebuild_segments_sets: Rebuild (stripe.go:410-412); async on stream. */
 int ec_rebuild_segments_sets(const ec_ctx *ctx, size_t nseg, const int *nshares, const int *nums,

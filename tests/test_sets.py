@@ -7,6 +7,7 @@ at once under prefetch, private/storage/streams/store.go:240-253).  Every
 output against the segment the oracle encoded; Decode's in-place correction
 against the oracle's pieces."""
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -125,6 +126,55 @@ def test_rebuild_sets_full_size_and_limits(oracle):
             assert np.array_equal(outs[g].cpu().numpy(), segs[g]), g
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("one", [1, 0])
+def test_rebuild_sets_one_segment(oracle, one):
+    """One segment per call (configs[2] as a single download runs it): one
+    launch with the rows solved on the host (rs_sets_one), or --
+    UPLINK_EC_SETS_ONE=0 -- the prep launch and the pass.  Full-size
+    RS(29,80) from all parity and from a random set; RS(128,256) (4 passes of
+    32 rows on 4 waves, past the one-launch limits: the two launches);
+    RS(40,100) (40 rows: 2 passes in one launch); RS(1,3);
+    all data present (no rows); a ragged last tile; one-segment calls
+    alternating on one context with many-segment calls (the slot's completion
+    counter each leaves at zero)."""
+    os.environ["UPLINK_EC_SETS_ONE"] = str(one)
+    try:
+        rng = np.random.default_rng(2 + one)
+        k, n, ess = 29, 80, 256
+        seg = oracle.pad(rng.integers(0, 256, 64 * 2**20, dtype=np.uint8), k * ess)
+        stripes = seg.size // (k * ess)
+        d_pieces = encode_all(oracle, k, n, ess, [seg])
+        c = Ctx(k, n, ess)
+        try:
+            for s in (list(range(n - k, n)), sorted(rng.choice(n, k, replace=False).tolist()), list(range(k))):
+                rc, outs = call_sets(c, d_pieces, [s], stripes)
+                assert rc == 0, _native.strerror(rc)
+                torch.cuda.synchronize()
+                assert np.array_equal(outs[0].cpu().numpy(), seg), s[:4]
+        finally:
+            c.close()
+        for k, n, stripes in ((128, 256, 3), (40, 100, 7), (1, 3, 20), (29, 80, 41), (20, 60, 130)):
+            segs = [rng.integers(0, 256, stripes * k * ess, dtype=np.uint8) for _ in range(3)]
+            d_pieces = encode_all(oracle, k, n, ess, segs)
+            c = Ctx(k, n, ess)
+            try:
+                for it in range(6):
+                    sets = random_sets(rng, k, n, 3, extra=it % 2)
+                    if it % 3 == 2:
+                        sets[0] = list(range(n - k, n))
+                    pick = [it % 3] if it % 2 == 0 else [0, 1, 2]
+                    rc, outs = call_sets(c, d_pieces[pick[0]:pick[-1] + 1], [sets[g] for g in pick], stripes)
+                    assert rc == 0, _native.strerror(rc)
+                    torch.cuda.synchronize()
+                    got = outs.cpu().numpy()
+                    for i, g in enumerate(pick):
+                        assert np.array_equal(got[i], segs[g]), (k, n, it, g)
+            finally:
+                c.close()
+    finally:
+        os.environ.pop("UPLINK_EC_SETS_ONE", None)
 
 
 def test_rebuild_sets_errors():

@@ -6,7 +6,9 @@ segment of a download comes with whichever 29 pieces answered first
   * batch: ec_rebuild_segments_sets, 32 RS(29,80) 64 MiB segments per call,
     32 fresh seeded 29-subsets per call; HIP-event time per call on the
     stream (launches back to back) and wall time per call.
-  * single: one segment, a fresh set, wall clock per call (launch + sync).
+  * single: one segment, a fresh set, wall clock per call (launch + sync), the
+    time until the call returns, and a one-element torch kernel's wall clock
+    (this box's floor for a launch and a synchronisation).
   * batched API (ec_rebuild_segments_batched) on a fresh set: first, second
     and warm launch of the set, wall clock, one segment and 16.
 Run on the GPU box: python tools/bench_sets.py [--reps N]"""
@@ -174,14 +176,23 @@ def main():
     assert L.ec_set_body(ctx, _native.EC_BODY_AUTO) == 0
     torch.cuda.synchronize()
     # single segment, fresh set, synchronous wall clock
-    walls = []
+    walls, calls, floor = [], [], []
+    tiny = torch.zeros(1, dtype=torch.int32, device=outs.device)
     for i in range(args.reps * 4):
         a1 = sets_args(fresh(1), outs)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sets_go(a1)
+        t1 = time.perf_counter()
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t0)
+        calls.append(t1 - t0)
+        # this box's floor for one launch and a synchronisation, as Python sees it
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tiny.add_(1)
+        torch.cuda.synchronize()
+        floor.append(time.perf_counter() - t0)
     ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     s1s = [sets_args(fresh(1), outs) for _ in range(args.reps)]
     torch.cuda.synchronize()
@@ -193,6 +204,8 @@ def main():
     b2b = ev2[0].elapsed_time(ev2[1]) * 1e-3 / args.reps
     res["single"] = {"wall_us_median": round(float(np.median(walls)) * 1e6, 1),
                      "wall_us_min": round(min(walls) * 1e6, 1),
+                     "call_returns_us_median": round(float(np.median(calls)) * 1e6, 1),
+                     "tiny_kernel_wall_us_median": round(float(np.median(floor)) * 1e6, 1),
                      "stream_us_back_to_back": round(b2b * 1e6, 1),
                      "frac_back_to_back": round(2 * SPAD / b2b / 1e9 / PEAK, 4)}
     # the batched single-set API on fresh sets: first / second / warm, wall clock

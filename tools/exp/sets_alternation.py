@@ -4,7 +4,10 @@ alternation than back to back: HIP-event time of one 32-segment
 ec_rebuild_segments_sets call (fresh sets) and of the warm straight-line
 rebuild of one set, each (a) back to back, (b) right after a full RS(29,80)
 encode launch, (c) right after a device copy of similar length, (d) after the
-GPU idled ~1.5 ms.  Prints one JSON line."""
+GPU idled ~1.5 ms, (e) right after a one-segment encode (every CU runs the
+encoder's code, 1/32 of its heat), (f) after a full encode and then a
+one-segment share-set decode (the leaves back in the instruction caches, the
+heat unchanged).  Prints one JSON line."""
 import ctypes
 import json
 import os
@@ -39,6 +42,9 @@ def main():
     def enc():
         assert L.ec_encode_segments(ctx, segs.data_ptr(), B, NSTRIPES, pcs.data_ptr(), 0, sp) == 0
 
+    def enc1():
+        assert L.ec_encode_segments(ctx, segs.data_ptr(), 1, NSTRIPES, pcs.data_ptr(), 0, sp) == 0
+
     def sets_args():
         sets = [sorted(int(x) for x in rng.permutation(N)[:K]) for _ in range(B)]
         flat = [x for s in sets for x in s]
@@ -50,6 +56,12 @@ def main():
     def dec_sets(i):
         a = pool[i % len(pool)]
         assert L.ec_rebuild_segments_sets(ctx, B, a[0], a[1], a[2], NSTRIPES, a[3], sp) == 0
+    s1 = sorted(int(x) for x in rng.permutation(N)[:K])
+    a1 = ((ctypes.c_int * 1)(K), (ctypes.c_int * K)(*s1), (ctypes.c_void_p * K)(*[pcs[1].data_ptr() + x * PLEN for x in s1]),
+          (ctypes.c_void_p * 1)(outs[1].data_ptr()))
+
+    def dec_sets1():
+        assert L.ec_rebuild_segments_sets(ctx, 1, a1[0], a1[1], a1[2], NSTRIPES, a1[3], sp) == 0
     one = sorted(int(x) for x in rng.permutation(N)[:K])
     cn = (ctypes.c_int * K)(*one)
     cptr = (ctypes.c_void_p * K)(*[pcs[0].data_ptr() + x * PLEN for x in one])
@@ -60,19 +72,27 @@ def main():
     def copy():
         cp_dst.copy_(cp_src)
 
+    def pre(mode):
+        if mode in ("after_encode", "after_encode_and_one_segment"):
+            enc()
+        elif mode == "after_copy":
+            copy()
+        elif mode == "after_small_encode":
+            enc1()
+        if mode == "after_encode_and_one_segment":
+            dec_sets1()
+
     enc()
     dec_sl(0)
     L.ec_prepare_rebuild(ctx, K, cn, 1)
     res = {}
     for name, dec in (("sets", dec_sets), ("straight_line", dec_sl)):
-        for mode in ("back_to_back", "after_encode", "after_copy", "after_idle"):
+        for mode in ("back_to_back", "after_encode", "after_copy", "after_idle", "after_small_encode",
+                     "after_encode_and_one_segment"):
             t_end = time.perf_counter() + 0.4
             i = 0
             while time.perf_counter() < t_end:  # settle in the same duty cycle
-                if mode == "after_encode":
-                    enc()
-                elif mode == "after_copy":
-                    copy()
+                pre(mode)
                 dec(i)
                 i += 1
                 if mode == "after_idle":
@@ -81,11 +101,8 @@ def main():
             torch.cuda.synchronize()
             per = []
             for r in range(16):
-                if mode == "after_encode":
-                    enc()
-                elif mode == "after_copy":
-                    copy()
-                elif mode == "after_idle":
+                pre(mode)
+                if mode == "after_idle":
                     torch.cuda.synchronize()
                     time.sleep(0.0015)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

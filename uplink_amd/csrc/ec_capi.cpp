@@ -606,6 +606,7 @@ int ec_create(int k, int n, int ess, ec_ctx **out) {
 #endif
     if (const char *e = getenv("UPLINK_EC_SETS_MERGE")) c->sets_merge = atoi(e) != 0;
     if (const char *e = getenv("UPLINK_EC_SETS_STAGE_DMA")) c->sets_stage_dma = atoi(e) != 0;
+    if (const char *e = getenv("UPLINK_EC_SETS_ONE")) c->sets_one = atoi(e) != 0;
     configure_rebuild(getenv("UPLINK_EC_REBUILD_DEPTH") ? atoi(getenv("UPLINK_EC_REBUILD_DEPTH")) : 1);
     if (const char *f = getenv("UPLINK_EC_FAULT_SINGLE"))
         if (sscanf(f, "max=%d,num=%d", &c->fault_max_batch, &c->fault_fail_num) != 2) c->fault_max_batch = 0;

@@ -422,6 +422,10 @@ struct ec_ctx {
     // writes to cached pinned memory; the stream then waits ~20 us for the copy engine between
     // calls, profiles/r05/g)
     bool sets_stage_dma = false;
+    // a one-segment Rebuild share-set call as one launch, its rows solved on the host and passed
+    // in the launch's arguments (rs_sets_one), instead of rs_sets_prep1 + rs_matmul_sets;
+    // UPLINK_EC_SETS_ONE=0 at ec_create for the two launches (A/B)
+    bool sets_one = true;
     SetsRing sets;
     SlBuilder slb;
 };

@@ -64,6 +64,32 @@ int set_segment(const ec_ctx *c, int nshares, const int *nums, const uint8_t *co
     return EC_OK;
 }
 
+// The rows of a Rebuild segment as rs_sets_prep solves them (rs_sets.hip,
+// closed-form Lagrange weights through the basis shares' points), into
+// coef[r * nin + j]: missing data position r from basis input j.
+void solve_rows_host(const SetSeg &sg, int k, uint8_t *coef) {
+    uint8_t x[kMaxOps];
+    int lw[kMaxOps];
+    for (int p = 0; p < k; p++) x[p] = gf_point(sg.num[p]);
+    for (int p = 0; p < k; p++) {
+        int l = 0;
+        for (int t = 0; t < k; t++)
+            if (t != p) l += kGf.log[x[p] ^ x[t]];
+        lw[p] = l % 255;
+    }
+    for (int r = 0; r < sg.nstore; r++) {
+        const uint8_t y = gf_point(sg.missing[r]);
+        int ln = 0, hit = -1;
+        for (int t = 0; t < k; t++) {
+            if (y == x[t]) hit = t;
+            else ln += kGf.log[y ^ x[t]];
+        }
+        for (int j = 0; j < k; j++)
+            coef[r * sg.nin + j] = hit >= 0 ? (uint8_t)(hit == j)
+                                            : kGf.exp[(((ln - kGf.log[y ^ x[j]] - lw[j]) % 255) + 255) % 255];
+    }
+}
+
 // The slots' host memory is read by rs_sets_prep and written by the launches'
 // last workgroup straight over the bus: coherent (uncached on the GPU side), so
 // a slot reused by the next call is never read from a stale cache line.
@@ -221,6 +247,46 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     const uint32_t seq = sl->seq + 1;
     const int64_t chunks = nstripes * (ess / 16), tiles = (chunks + kTileChunksHost - 1) / kTileChunksHost;
     hipError_t e = hipSuccess;
+    if (in_args && !bad && c->sets_one && segs[0].nin <= kOneMaxIn && segs[0].nin * segs[0].rows <= kOneMaxCoef) {
+        // one segment, one launch: its rows solved here, its record and coefficients in the
+        // launch's arguments
+        const SetSeg &sg = segs[0];
+        SetOne p{};
+        p.a.nstripes = nstripes;
+        p.a.chunks_per_seg = chunks;
+        p.a.tiles_per_seg = tiles;
+        p.a.total_tiles = tiles;
+        p.a.ess = ess;
+        p.a.cps = ess / 16;
+        p.a.k = k;
+        p.a.done_ctr = sl->d_words;
+        p.a.host_done = sl->h_words;
+        p.a.seq = seq;
+        p.a.total_wgs = (uint32_t)tiles;
+        p.a.chk_flag = c->d_chk;
+        p.a.jt_base = c->jt_base;
+        for (int j = 0; j < sg.nin; j++) {
+            p.in[j] = one.d.in[j];
+            p.copy_off[j] = one.d.copy_off[j];
+        }
+        for (int r = 0; r < sg.nstore; r++) p.out_off[r] = one.d.out_off[r];
+        p.out = sg.out;
+        p.tgt = sl->d_tgt;
+        p.nin = sg.nin;
+        p.nout = sg.rows;
+        p.nstore = sg.nstore;
+        solve_rows_host(sg, k, p.coef);
+        e = launch_sets_one(p, sg.nw, s);
+        if (e != hipSuccess) {  // nothing was queued
+            sets_release(c, sl);
+            return hip_fail(e);
+        }
+        sl->seq = seq;
+        c->last_body = EC_BODY_JUMP_TABLE;
+        const int rc = after_launch(c->d_chk, s);
+        sets_release(c, sl);
+        return rc;
+    }
     if (sl->d_stage)  // (the host's writes went to cached memory; one DMA takes them to the device)
         e = hipMemcpyAsync(sl->d_stage, sl->h_stage, nseg * sizeof(SetStage), hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
@@ -256,7 +322,9 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
         // word will never be written: once the stream has run what was queued, the
         // slot is free again (the next call's prep zeroes its counter); if the
         // device does not get there, the slot is never reused
-        const bool drained = hipStreamSynchronize(s) == hipSuccess;
+        // (a one-segment pass, rs_sets_one, relies on the completion counter being zero: a pass that ran
+        // in part left it counting)
+        const bool drained = hipStreamSynchronize(s) == hipSuccess && hipMemset(sl->d_words, 0, 4) == hipSuccess;
         std::lock_guard<std::mutex> g(c->sets.mu);
         sl->dead = !drained;
         sl->busy = false;

@@ -47,7 +47,9 @@ __device__ __forceinline__ void rows_of(int pass, int npass, int nout, int nw, i
 
 __device__ __forceinline__ int npass_of(int nout, int nw) { return nout > 0 ? (nout + nw * kRows - 1) / (nw * kRows) : 1; }
 
-__device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64_t jt_base, uint32_t *done_ctr) {
+// One segment's decode rows, solved and written as leaf addresses by one
+// workgroup (rs_sets_prep).
+__device__ __forceinline__ void solve_rows(const SetStage *st, uint64_t jt_base) {
     __shared__ uint8_t s_exp[512], s_log[256];
     __shared__ uint8_t s_x[kMaxOps];                    // basis points x_p
     __shared__ uint8_t s_y[2 * kMaxOps];                // row points y_r
@@ -57,17 +59,10 @@ __device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64
     __shared__ int s_acc[kMaxOps + 2 * kMaxOps];  // the sums of logarithms of W_p, then of N_r
     __shared__ int s_hdr[8];
     __shared__ uint64_t *s_tgt;
-    const int tid = threadIdx.x;
-    // everything from the host's staging at once (one round trip over the bus, or the kernel's
-    // arguments)
-    {
-        const uint64_t *src = (const uint64_t *)&st->d;
-        uint64_t *dst = (uint64_t *)dd;
-        for (int i = tid; i < (int)(sizeof(SetDesc) / 8); i += blockDim.x) dst[i] = src[i];
-    }
-    if (tid < kMaxOps) {
-        s_num[tid] = st->num[tid];
-        s_miss[tid] = st->missing[tid];
+    const int tid = threadIdx.x, nt = (int)blockDim.x;
+    for (int i = tid; i < kMaxOps; i += nt) {
+        s_num[i] = st->num[i];
+        s_miss[i] = st->missing[i];
     }
     if (tid == 0) s_hdr[0] = st->d.nin;
     if (tid == 1) s_hdr[1] = st->d.nout;
@@ -75,31 +70,25 @@ __device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64
     if (tid == 3) s_hdr[3] = st->nw;
     if (tid == 4) s_hdr[4] = st->k;
     if (tid == 5) s_tgt = st->d.tgt;
-    if (tid == 6) {
-        uint32_t *zc = st->d.zero_check;
-        if (zc) *zc = 0u;
-    }
-    if (tid == 7 && blockIdx.x == 0 && done_ctr) *done_ctr = 0u;
-    for (int i = tid; i < 512; i += blockDim.x) s_exp[i] = c_gf.exp[i];
-    for (int i = tid; i < 256; i += blockDim.x) s_log[i] = c_gf.log[i];
+    for (int i = tid; i < 512; i += nt) s_exp[i] = c_gf.exp[i];
+    for (int i = tid; i < 256; i += nt) s_log[i] = c_gf.log[i];
     __syncthreads();
     const int nin = s_hdr[0], nout = s_hdr[1], nstore = s_hdr[2], nw = s_hdr[3], k = s_hdr[4];
     auto point = [&](int num) -> uint8_t { return num == 0 ? 0 : s_exp[(num - 1) % 255]; };
-    if (tid < k) s_x[tid] = point(s_num[tid]);
+    for (int i = tid; i < k; i += nt) s_x[i] = point(s_num[i]);
     // row r's point: a missing data position (its data index), or a non-basis share (a syndrome row)
-    if (tid < nout) s_y[tid] = point(tid < nstore ? s_miss[tid] : s_num[k + tid - nstore]);
-    __syncthreads();
+    for (int i = tid; i < nout; i += nt) s_y[i] = point(i < nstore ? s_miss[i] : s_num[k + i - nstore]);
     // log W_p = sum over t != p of log(x_p ^ x_t) (the points are distinct: the host checked), and
     // log N_r = sum over t of log(y_r ^ x_t), a row whose point is a basis point being that share
     // itself: (k + nout) x k independent terms, spread over the workgroup and added in LDS
     // (one term per thread and step instead of a k-long chain per sum: 13 -> ~5 us per launch)
-    if (tid < k) s_acc[tid] = 0;
-    if (tid < nout) {
-        s_acc[kMaxOps + tid] = 0;
-        s_hit[tid] = -1;
+    for (int i = tid; i < k; i += nt) s_acc[i] = 0;
+    for (int i = tid; i < nout; i += nt) {
+        s_acc[kMaxOps + i] = 0;
+        s_hit[i] = -1;
     }
     __syncthreads();
-    for (int e = tid; e < (k + nout) * k; e += blockDim.x) {
+    for (int e = tid; e < (k + nout) * k; e += nt) {
         const int a = e / k, t = e - a * k;
         if (a < k) {
             if (t != a) atomicAdd(&s_acc[a], (int)s_log[s_x[a] ^ s_x[t]]);
@@ -110,15 +99,15 @@ __device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64
         }
     }
     __syncthreads();
-    if (tid < k) s_lw[tid] = (int16_t)(s_acc[tid] % 255);
-    if (tid < nout) s_ln[tid] = (int16_t)(s_acc[kMaxOps + tid] % 255);
+    for (int i = tid; i < k; i += nt) s_lw[i] = (int16_t)(s_acc[i] % 255);
+    for (int i = tid; i < nout; i += nt) s_ln[i] = (int16_t)(s_acc[kMaxOps + i] % 255);
     __syncthreads();
     // leaf addresses: coefficient of basis input j in row r is N_r / ((y_r ^ x_j) W_j) (Lagrange
     // interpolation through the basis points, evaluated at y_r); 1 on a non-basis input's own
     // syndrome row; else 0
     const int npass = npass_of(nout, nw), per_pass = nin * nw * kRows;
     uint64_t *tgt = s_tgt;
-    for (int e = tid; e < npass * per_pass; e += blockDim.x) {
+    for (int e = tid; e < npass * per_pass; e += nt) {
         const int pass = e / per_pass, rem = e - pass * per_pass;
         const int j = rem / (nw * kRows), g = (rem / kRows) % nw, o = rem % kRows;
         int rb, cn;
@@ -138,6 +127,23 @@ __device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64
         }
         tgt[e] = jt_base + (uint64_t)c * RS_JT_SLOT;
     }
+}
+
+__device__ __forceinline__ void prep_one(const SetStage *st, SetDesc *dd, uint64_t jt_base, uint32_t *done_ctr) {
+    const int tid = threadIdx.x;
+    // the descriptor from the host's staging at once (one round trip over the bus, or the
+    // kernel's arguments)
+    {
+        const uint64_t *src = (const uint64_t *)&st->d;
+        uint64_t *dst = (uint64_t *)dd;
+        for (int i = tid; i < (int)(sizeof(SetDesc) / 8); i += blockDim.x) dst[i] = src[i];
+    }
+    if (tid == 6) {
+        uint32_t *zc = st->d.zero_check;
+        if (zc) *zc = 0u;
+    }
+    if (tid == 7 && blockIdx.x == 0 && done_ctr) *done_ctr = 0u;
+    solve_rows(st, jt_base);
 }
 
 __global__ __launch_bounds__(256) void rs_sets_prep(const SetStage *stage, SetDesc *desc, uint64_t jt_base,
@@ -170,8 +176,17 @@ __device__ __forceinline__ bool in_span(const SetsArgs &a, const uint8_t *p, con
 // the K$) -- the jump-table body needs its leaf-table address in SGPRs.
 typedef const __attribute__((address_space(4))) SetDesc ConstDesc;
 
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
+typedef const __attribute__((address_space(4))) SetOne ConstOne;
+
+// One tile of a share-set pass; D: ConstDesc (the segment's descriptor in
+// device memory, its leaf table made by rs_sets_prep) or ConstOne (one segment,
+// rs_sets_one: the record is the launch's arguments, and the workgroup writes
+// the leaf table from the host's coefficients while its first chunk's loads
+// are in flight -- every workgroup the same bytes -- and reads it back with
+// scalar loads once its own stores are complete).
+template <int NW, class D>
+__device__ __forceinline__ void sets_tile(const SetsArgs &a, D *d) {
+    constexpr bool ONE = __is_same(D, ConstOne);
     constexpr int JC = 2 * NW, PER = 2, OPW = kRows, SLOT = JC * 2048;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     u32x4 *ring = (u32x4 *)smem;
@@ -180,8 +195,7 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
     const int group = (wave + (int)(blockIdx.x % NW)) % NW;
     const uint32_t ring_addr = (uint32_t)(uintptr_t)smem;
     const int64_t tile = blockIdx.x;
-    const int64_t seg = tile / a.tiles_per_seg;
-    ConstDesc *d = (ConstDesc *)(a.desc + seg);
+    const int64_t seg = ONE ? 0 : tile / a.tiles_per_seg;
     const int nin = d->nin, nout = d->nout;
     const int64_t piece_len = a.nstripes * a.ess, spad = piece_len * a.k;
     if (d->status == 0 && nin > 0) {
@@ -218,13 +232,28 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
             }
         };
         uint8_t *out = d->out;
+        if constexpr (ONE) {
+            // (the table's stores are waited for with the chunk's loads, before the barrier every
+            // wave passes ahead of its first scalar load of the table)
+            issue(0);
+            uint64_t *t = d->tgt;
+            for (int e = threadIdx.x; e < npass * nin * NW * OPW; e += NW * 64) {
+                const int pass = e / (nin * NW * OPW), rem = e - pass * (nin * NW * OPW);
+                const int j = rem / (NW * OPW), g = (rem / OPW) % NW, o = rem % OPW;
+                int rb, cn;
+                rows_of(pass, npass, nout, NW, g, rb, cn);
+                const int oo = o - (OPW - cn);
+                const uint32_t c = oo >= 0 ? d->coef[(rb + oo) * nin + j] : 0u;
+                t[e] = a.jt_base + (uint64_t)c * RS_JT_SLOT;
+            }
+        }
         for (int pass = 0; pass < npass; pass++) {
             int rbase, cnt;
             rows_of(pass, npass, nout, NW, group, rbase, cnt);
+            if (!ONE || pass > 0) issue(0);
             u32x8 acc[OPW];
 #pragma unroll
             for (int o = 0; o < OPW; o++) acc[o] = (u32x8){0, 0, 0, 0, 0, 0, 0, 0};
-            issue(0);
             for (int ch = 0; ch < nchunks; ch++) {
                 wait_vm(0);
                 const int j0 = ch * CH;
@@ -302,6 +331,16 @@ __global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
     }
 }
 
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 4) void rs_matmul_sets(const SetsArgs a) {
+    sets_tile<NW>(a, (ConstDesc *)(a.desc + blockIdx.x / a.tiles_per_seg));
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 4) void rs_sets_one(const SetOne p) {
+    sets_tile<NW>(p.a, (ConstOne *)&p);
+}
+
 }  // namespace
 
 // as the straight-line split (rs_sl_codegen.cpp split_for): 15-16 rows on 3 waves, not 2 -- one
@@ -327,6 +366,20 @@ hipError_t launch_sets_prep(const SetStage *stage, SetDesc *desc, int nseg, uint
 hipError_t launch_sets_prep1(const SetStage &stage, SetDesc *desc, uint64_t jt_base, uint32_t *done_ctr,
                              hipStream_t s) {
     hipLaunchKernelGGL(rs_sets_prep1, dim3(1), dim3(256), 0, s, stage, desc, jt_base, done_ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_sets_one(const SetOne &p, int nw, hipStream_t s) {
+    if (p.a.total_tiles <= 0) return hipSuccess;
+    if (p.a.total_tiles > sets_max_tiles(nw) || p.nin > kOneMaxIn || p.nin * p.nout > kOneMaxCoef)
+        return hipErrorInvalidValue;
+    const dim3 grid((unsigned)p.a.total_tiles);
+    switch (nw) {
+    case 2: hipLaunchKernelGGL(rs_sets_one<2>, grid, dim3(2 * 64), (size_t)2 * 4 * 2048, s, p); break;
+    case 3: hipLaunchKernelGGL(rs_sets_one<3>, grid, dim3(3 * 64), (size_t)2 * 6 * 2048, s, p); break;
+    case 4: hipLaunchKernelGGL(rs_sets_one<4>, grid, dim3(4 * 64), (size_t)2 * 8 * 2048, s, p); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ struct SetsArgs {
     uint32_t *host_done;
     uint32_t seq, total_wgs;
     uint32_t *chk_flag;  // checked build: first access outside a share / segment (site 8 or 9)
+    uint64_t jt_base;    // rs_sets_fused1: address of leaf 0
 };
 
 constexpr int64_t kTileChunksHost = 128;  // 16-byte chunks per tile (rs_tile.hpp kTileChunks)
@@ -74,6 +75,26 @@ hipError_t launch_sets_prep1(const SetStage &stage, SetDesc *desc, uint64_t jt_b
                              hipStream_t s);
 static_assert(sizeof(SetStage) + 3 * sizeof(void *) <= 4096, "a launch's arguments are at most 4 KB");
 hipError_t launch_matmul_sets(const SetsArgs &a, int nw, hipStream_t s);
+
+// One segment's Rebuild in one launch (rs_sets_one): its record and its decode
+// rows' coefficients, solved on the host, are the launch's arguments; every
+// workgroup writes the leaf table (the same bytes) and reads it back.  Field
+// names as SetDesc's (the tile body reads either).
+constexpr int kOneMaxIn = 64, kOneMaxCoef = 2048;
+struct SetOne {
+    SetsArgs a;
+    const uint8_t *in[kOneMaxIn];
+    uint8_t *out;
+    uint64_t *tgt;         // the leaf table [pass][input][group][8]
+    uint32_t *zero_check;  // null (Rebuild)
+    int32_t nin, nout, nstore, status;
+    int32_t copy_off[kOneMaxIn];
+    int32_t out_off[kOneMaxIn];
+    uint8_t coef[kOneMaxCoef];  // coef[r * nin + j]: row r's coefficient of input j
+};
+static_assert(sizeof(SetOne) <= 4096, "a launch's arguments are at most 4 KB");
+// *p.a.done_ctr must be 0 (every pass leaves it so)
+hipError_t launch_sets_one(const SetOne &p, int nw, hipStream_t s);
 // address of the jump table's leaf 0 on the current device (one small launch on
 // s, synchronous; the table sits in rs_jt_targets' code)
 hipError_t jt_table_base_addr(uint64_t *out, hipStream_t s);
