@@ -218,6 +218,20 @@ static void share_sets_surface(int k, int n, int ess) {
     CHECK(ec_copy(back, d_out, NSEG * spad) == EC_OK, "ec_copy D2H");
     for (int g = 0; g < NSEG; g++)
         CHECK(memcmp(back + g * spad, segs + g * spad, spad) == 0, "sets rebuild: segment %d != input (%d,%d)", g, k, n);
+    /* the same sets one segment per call (a lone download's segment: one launch, rows solved on the host) */
+    {
+        uint8_t *zero = calloc(NSEG * spad, 1);
+        CHECK(ec_copy(d_out, zero, NSEG * spad) == EC_OK, "clear outputs");
+        free(zero);
+        for (int g = 0, off = 0; g < NSEG; off += ns[g], g++) {
+            rc = ec_rebuild_segments_sets(ctx, 1, ns + g, nums + off, ptrs + off, stripes, outs + g, NULL);
+            CHECK(rc == EC_OK, "ec_rebuild_segments_sets (one segment) rc %d (%s)", rc, ec_strerror(rc));
+        }
+        CHECK(ec_copy(back, d_out, NSEG * spad) == EC_OK, "ec_copy D2H");
+        for (int g = 0; g < NSEG; g++)
+            CHECK(memcmp(back + g * spad, segs + g * spad, spad) == 0, "sets rebuild, one per call: segment %d (%d,%d)", g,
+                  k, n);
+    }
     if (n - k >= 2) {
         /* Decode: k + 2 shares per segment, segment 1's second share corrupted in one byte */
         uint8_t *dptr[NSEG * 256];
