@@ -197,13 +197,15 @@ def test_rebuild_sets_errors():
         c.close()
 
 
-def test_rebuild_sets_many_calls_streams_and_threads(oracle):
+@pytest.mark.parametrize("nseg", [6, 1])
+def test_rebuild_sets_many_calls_streams_and_threads(oracle, nseg):
     """More calls in flight than the context's 16 slots, from 4 threads on 4
     streams: a slot is reused only once the GPU has finished the call that
     used it (its last workgroup's completion word), so every segment of every
-    call is rebuilt from its own set."""
-    k, n, ess, stripes, nseg = 29, 80, 256, 64, 6
-    rng = np.random.default_rng(16)
+    call is rebuilt from its own set.  nseg = 1: every call the one-launch
+    pass, whose leaf table lives in the slot too."""
+    k, n, ess, stripes = 29, 80, 256, 64
+    rng = np.random.default_rng(16 + nseg)
     segs = [rng.integers(0, 256, stripes * k * ess, dtype=np.uint8) for _ in range(nseg)]
     d_pieces = encode_all(oracle, k, n, ess, segs)
     c = Ctx(k, n, ess)
