@@ -233,8 +233,12 @@ __device__ __forceinline__ void sets_tile(const SetsArgs &a, D *d) {
         };
         uint8_t *out = d->out;
         if constexpr (ONE) {
-            // (the table's stores are waited for with the chunk's loads, before the barrier every
-            // wave passes ahead of its first scalar load of the table)
+            // Every workgroup writes the whole table, the same bytes, and reads it only after its
+            // own stores are complete: the chunk's vmcnt(0) below waits for them with the loads,
+            // before the barrier every wave passes ahead of its first scalar load of the table.
+            // Whichever copy a read meets -- this XCD's L2 line, or the scalar cache's, filled by
+            // a workgroup that had itself finished writing -- holds these bytes; the scalar cache
+            // starts the launch empty, so nothing is left from the slot's previous call.
             issue(0);
             uint64_t *t = d->tgt;
             for (int e = threadIdx.x; e < npass * nin * NW * OPW; e += NW * 64) {
