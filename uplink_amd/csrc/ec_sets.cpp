@@ -246,25 +246,29 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
     }
     const uint32_t seq = sl->seq + 1;
     const int64_t chunks = nstripes * (ess / 16), tiles = (chunks + kTileChunksHost - 1) / kTileChunksHost;
+    // a pass's arguments, but for its segments (desc, total_tiles)
+    auto pass_args = [&](SetsArgs &a) {
+        a.nstripes = nstripes;
+        a.chunks_per_seg = chunks;
+        a.tiles_per_seg = tiles;
+        a.ess = ess;
+        a.cps = ess / 16;
+        a.k = k;
+        a.done_ctr = sl->d_words;
+        a.host_done = sl->h_words;
+        a.seq = seq;
+        a.total_wgs = (uint32_t)(tiles * (int64_t)nseg);
+        a.chk_flag = c->d_chk;
+        a.jt_base = c->jt_base;
+    };
     hipError_t e = hipSuccess;
     if (in_args && !bad && c->sets_one && segs[0].nin <= kOneMaxIn && segs[0].nin * segs[0].rows <= kOneMaxCoef) {
         // one segment, one launch: its rows solved here, its record and coefficients in the
         // launch's arguments
         const SetSeg &sg = segs[0];
         SetOne p{};
-        p.a.nstripes = nstripes;
-        p.a.chunks_per_seg = chunks;
-        p.a.tiles_per_seg = tiles;
+        pass_args(p.a);
         p.a.total_tiles = tiles;
-        p.a.ess = ess;
-        p.a.cps = ess / 16;
-        p.a.k = k;
-        p.a.done_ctr = sl->d_words;
-        p.a.host_done = sl->h_words;
-        p.a.seq = seq;
-        p.a.total_wgs = (uint32_t)tiles;
-        p.a.chk_flag = c->d_chk;
-        p.a.jt_base = c->jt_base;
         for (int j = 0; j < sg.nin; j++) {
             p.in[j] = one.d.in[j];
             p.copy_off[j] = one.d.copy_off[j];
@@ -301,19 +305,9 @@ int sets_call(ec_ctx *c, std::vector<SetSeg> &segs, int64_t nstripes, hipStream_
         size_t q1 = q0;
         while (q1 < nseg && segs[idx[q1]].nw == segs[idx[q0]].nw) q1++;
         SetsArgs a{};
+        pass_args(a);
         a.desc = sl->d_desc + q0;
-        a.nstripes = nstripes;
-        a.chunks_per_seg = chunks;
-        a.tiles_per_seg = tiles;
         a.total_tiles = tiles * (int64_t)(q1 - q0);
-        a.ess = ess;
-        a.cps = ess / 16;
-        a.k = k;
-        a.done_ctr = sl->d_words;
-        a.host_done = sl->h_words;
-        a.seq = seq;
-        a.total_wgs = (uint32_t)(tiles * (int64_t)nseg);
-        a.chk_flag = c->d_chk;
         e = launch_matmul_sets(a, segs[idx[q0]].nw, s);
         q0 = q1;
     }
