@@ -2,8 +2,8 @@
 """Effective shader clock per dispatch from a rocprofv3 --pmc GRBM_GUI_ACTIVE
 --kernel-trace run: GRBM_GUI_ACTIVE (summed over the 8 XCDs, so / 8) over the
 dispatch's duration.  With --context, each dispatch of the named kernel is
-labelled by the kernel dispatched before it (and a gap > 1 ms before it is
-labelled "idle").  Prints one JSON line: median clock (GHz) per (kernel,
+labelled by the kernel dispatched before it, skipping rs_sets_prep (and a
+gap > 1 ms before it is labelled "idle").  Prints one JSON line: median clock (GHz) per (kernel,
 context), with counts.
 
 usage: clock_by_kernel.py RUN_DIR [--kernel SUBSTR ...] [--context]"""
@@ -44,7 +44,8 @@ def main():
         if (not a.kernel or any(k in name for k in a.kernel)) and t1 > t0:
             key = short(name) + (" after " + short(ctx) if a.context else "")
             out.setdefault(key, []).append(v / 8 / (t1 - t0))
-        prev_end, prev_name = t1, name
+        if "rs_sets_prep" not in name:  # (the share-set pass's own prep is not its context)
+            prev_end, prev_name = t1, name
     print(json.dumps({k: {"ghz_median": round(statistics.median(x), 3), "n": len(x)} for k, x in sorted(out.items())}))
 
 
